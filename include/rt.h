@@ -1,0 +1,190 @@
+/*
+ * rt.h — C-ABI of the MI355X per-pixel ray tracer (libopenglraytracer_amd.so).
+ *
+ * Drop-in for the reference's frame-driver -> compute-shader boundary:
+ *
+ *   reference (OpenGLRaytracer/main.cpp)          this ABI
+ *   ------------------------------------------    ------------------------------
+ *   :203 createShaderProgram("raytrace_compute")  rt_create()           (once)
+ *   :129-159 RGBA8 W x H texture (host-owned)     caller-owned float4 buffer
+ *   raytrace_compute.glsl:74-321 scene consts     rt_scene_create()     (per scene/time)
+ *   :213 get_current_time(), :226 uniform time    `time` argument
+ *   :223 glBindImageTexture + :235 glDispatch     rt_render()
+ *   :238 glFinish                                 rt_render() with stream == NULL
+ *
+ * All structs are plain C, float32, no padding surprises (4-byte members
+ * only). Every entry point returns RT_OK (0) or a negative RT_ERR_* code and
+ * never throws across the boundary; rt_last_error() returns a thread-local
+ * message for the last failure on the calling thread.
+ *
+ * Output layout (identical to the reference image, raytrace_compute.glsl:404):
+ * row-major, row 0 = y 0 (GL's bottom row), pixel (x, y) at index y*W + x,
+ * 4 floats (r, g, b, 0) per pixel, unclamped (the shipped RGBA8 surface
+ * clamps; rt_pack_rgba8 reproduces that).
+ */
+#ifndef OPENGLRAYTRACER_AMD_RT_H
+#define OPENGLRAYTRACER_AMD_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_ERR_INVALID (-1)     /* bad argument */
+#define RT_ERR_HIP (-2)         /* HIP runtime error */
+#define RT_ERR_NOMEM (-3)       /* allocation failed */
+#define RT_ERR_UNSUPPORTED (-4) /* e.g. max_depth above RT_MAX_DEPTH */
+#define RT_ERR_NO_DEVICE (-5)   /* no GPU / bad device index */
+
+/* Deepest recursion compiled into the kernel. The reference's stack machine
+ * (raytrace_compute.glsl:873-874,1077-1101) holds 100 elements and gives up
+ * after 10000 steps; with at most 2^(D+1)-1 traced rays of 6 steps each the
+ * step guard cannot trigger for D <= 9, so results are exact up to here. */
+#define RT_MAX_DEPTH 9
+
+/* raytrace_compute.glsl:56-69 Material */
+typedef struct rt_material {
+    float ambient[4];
+    float diffuse[4];
+    float specular[4];
+    float shininess;
+    float emissive[4];
+    float reflectivity;
+    float transparency;
+    float refraction_index;
+} rt_material;
+
+/* raytrace_compute.glsl:244-258 Object (Box :166-170, Sphere :172-175).
+ * Type test exactly as get_closest_collision (:749-771): a box when
+ * box_mins/box_maxs are not both (0,0,0) (null_box, :178); otherwise a sphere
+ * when radius != -1 (null_sphere, :179); otherwise skipped. */
+typedef struct rt_object {
+    float box_mins[3];
+    float box_maxs[3];
+    float radius;
+    float position[3];
+    float angles[3]; /* pitch, yaw, roll in degrees (:254) */
+    int32_t material; /* index into the scene's material table */
+} rt_object;
+
+/* raytrace_compute.glsl:190-196 Light (point light, Phong terms) */
+typedef struct rt_light {
+    float position[3];
+    float ambient[4];
+    float diffuse[4];
+    float specular[4];
+} rt_light;
+
+/* raytrace_compute.glsl:36-50 Camera */
+typedef struct rt_camera {
+    float position[3];
+    float angles[3]; /* pitch, yaw, roll in degrees */
+    float v_fov;     /* degrees */
+    float aspect;    /* the reference fixes 16/9 whatever W/H is (:363) */
+    float near_plane;
+    float far_plane;
+} rt_camera;
+
+/* The per-frame camera constants the kernel consumes: the column-major
+ * inverse(proj * view) that unprojects NDC (:383) and the ray origin, the
+ * camera position (:391). rt_make_view derives it from an rt_camera in
+ * float64 (rounded once to float32); callers may also supply their own
+ * (e.g. a value another renderer computed). */
+typedef struct rt_view {
+    float unprojection[16];
+    float origin[3];
+} rt_view;
+
+typedef struct rt_context rt_context; /* one per device; not thread-safe */
+typedef struct rt_scene rt_scene;     /* device-resident, precomputed scene */
+
+/* ---- reference scene / camera (host functions, no GPU) --------------- */
+
+/* The 7 materials of raytrace_compute.glsl:74-157, in this order:
+ * material1, material2, red_glass, green_glass, blue_glass, mirror, wall. */
+#define RT_MAT_MATERIAL1 0
+#define RT_MAT_MATERIAL2 1
+#define RT_MAT_RED_GLASS 2
+#define RT_MAT_GREEN_GLASS 3
+#define RT_MAT_BLUE_GLASS 4
+#define RT_MAT_MIRROR 5
+#define RT_MAT_WALL 6
+#define RT_REFERENCE_MATERIALS 7
+#define RT_REFERENCE_LIGHTS 3
+#define RT_REFERENCE_OBJECTS 5
+
+int rt_reference_materials(rt_material out[RT_REFERENCE_MATERIALS]);
+/* raytrace_compute.glsl:199-224 */
+int rt_reference_lights(rt_light out[RT_REFERENCE_LIGHTS]);
+/* raytrace_compute.glsl:236-237,261-321: the shipped, time-animated scene. */
+int rt_reference_objects(float time, rt_object out[RT_REFERENCE_OBJECTS]);
+/* raytrace_compute.glsl:334-364: the orbiting camera at `time`. */
+int rt_reference_camera(float time, rt_camera *out);
+/* Benchmark scenes: object 0 is the reference room box
+ * (+-11, wall material); then n_spheres seeded spheres (splitmix64 stream,
+ * centre U([-8,8]x[-8,8]x[-4,4]), radius U(0.3,1.2), materials cycling
+ * material1, material2, red_glass, green_glass, blue_glass, mirror).
+ * `out` holds n_spheres + 1 objects. */
+int rt_bench_objects(int n_spheres, uint64_t seed, rt_object *out);
+
+/* cam == NULL: the reference orbit camera at `time`. */
+int rt_make_view(const rt_camera *cam, float time, rt_view *out);
+
+/* ---- device API ------------------------------------------------------ */
+int rt_create(int device, rt_context **out);
+void rt_destroy(rt_context *ctx);
+
+/* Copies and precomputes (transforms, inverse transforms, normal matrices)
+ * the scene and uploads it to the context's device. Arrays are host memory
+ * and may be freed after the call. n_objs <= RT_MAX_OBJECTS. */
+#define RT_MAX_OBJECTS 1024
+#define RT_MAX_LIGHTS 16
+#define RT_MAX_MATERIALS 256
+int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt_material *mats,
+                    int n_mats, const rt_light *lights, int n_lights, rt_scene **out);
+void rt_scene_destroy(rt_scene *scene);
+
+/* Render rows [row_begin, row_end) of a width x height frame.
+ *  cam        NULL = the reference orbit camera at `time` (main(), :334-364).
+ *  out        (row_end-row_begin)*width*4 floats; device memory of this
+ *             context's GPU if out_is_device, else host memory.
+ *  hip_stream hipStream_t; NULL = the context's own stream and the call
+ *             returns after the frame is complete (the reference's glFinish,
+ *             main.cpp:238). A non-NULL stream makes the call asynchronous
+ *             (out_is_device must then be 1).
+ * No allocation happens here after the first call at a given size. */
+int rt_render(rt_context *ctx, const rt_scene *scene, const rt_camera *cam, float time, int width,
+              int height, int max_depth, int row_begin, int row_end, float *out, int out_is_device,
+              void *hip_stream);
+
+/* Same, with explicit frame constants. */
+int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width, int height,
+                   int max_depth, int row_begin, int row_end, float *out, int out_is_device,
+                   void *hip_stream);
+
+/* Row-block interleaved shard for multi-GPU frames: renders the rows r of the
+ * frame with (r / block_rows) % n_shards == shard, in increasing order, packed
+ * densely into out_device (rt_shard_rows() rows of width*4 floats). */
+int rt_shard_rows(int height, int block_rows, int n_shards, int shard);
+int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width,
+                    int height, int max_depth, int block_rows, int n_shards, int shard,
+                    float *out_device, void *hip_stream);
+
+/* Kernel-only timing of the last rt_render/rt_render_shard on the context's
+ * stream (ms, from HIP events around the launch). */
+int rt_last_kernel_ms(rt_context *ctx, float *ms);
+
+/* RGBA8 unorm packing of a float frame as the shipped GL_RGBA8 surface stores
+ * it (clamp to [0,1], round to nearest). Host memory, n pixels. */
+int rt_pack_rgba8(const float *rgba32f, size_t n_pixels, uint8_t *out_rgba8);
+
+const char *rt_last_error(void);
+const char *rt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,106 @@
+// rt_internal.h — shared declarations of the product library (host side).
+//
+// Layout of the device-resident scene (one hipMalloc'd blob per rt_scene, see
+// rt_scene.cpp) and the per-launch parameter block consumed by the kernel in
+// rt_kernel.hip. Everything is float32 / int32; offsets are in 16-byte units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/rt.h"
+
+namespace rtamd {
+
+// One sphere of the closest-hit loop: centre and radius*radius (the float
+// product raytrace_compute.glsl:588 forms), 16 B.
+struct SphereRec {
+    float cx, cy, cz, rr;
+};
+// Identity of a sphere: its index in the reference object order (tie-break
+// of get_closest_collision, :773) and its material.
+struct SphereMeta {
+    int32_t obj_index;
+    int32_t material;
+    float radius;  // kept for completeness (intersection uses rr)
+    int32_t pad;
+};
+
+// One oriented box (:647-724) with its frame constants precomputed once per
+// scene: world_to_local (:652), local_to_world (:650) and the normal matrix
+// transpose(inverse(mat3(L))) (:718). Matrices are row-major 3x4 (the x/y/z
+// rows of the GLSL mat4; the w row of an affine transform is (0,0,0,1)).
+struct BoxRec {
+    float w2l[12];
+    float l2w[12];
+    float nrm[9];
+    float mins[3];
+    float maxs[3];
+    int32_t obj_index;
+    int32_t material;
+    int32_t pad[3];
+};  // 48 floats = 192 B
+static_assert(sizeof(BoxRec) == 192, "BoxRec layout");
+
+// Material (:56-69) plus the per-material light products the shading loop
+// would otherwise recompute: amb_sum = sum_j La_j * Ma (:801, same order),
+// and for each light j: Ld_j * Md (:830), Ls_j * Ms (:832).
+struct MatRec {
+    float amb_sum[4];
+    float emissive[4];
+    float shininess, reflectivity, transparency, refraction_index;
+};  // 48 B
+struct LightMatRec {
+    float ld_md[4];
+    float ls_ms[4];
+};  // 32 B
+struct LightRec {
+    float pos[3];
+    float pad;
+};
+
+// Per-launch parameters (kernarg, read through the scalar cache).
+struct LaunchParams {
+    float unproj[16];  // column-major inverse(proj*view) (:383)
+    float origin[3];   // ray start = camera position (:391)
+    int32_t width, height;
+    int32_t row_begin, n_rows;          // contiguous band [row_begin, row_begin+n_rows)
+    int32_t block_rows, n_shards, shard;  // interleaved shard mapping when n_shards > 0
+    int32_t n_spheres, n_boxes, n_mats, n_lights;
+    const void *scene;  // device blob
+    float4 *out;        // n_rows * width float4
+    int32_t off_spheres, off_smeta, off_boxes, off_mats, off_lights, off_lightmat;  // 16-B units
+    int32_t blob_units;                                                         // blob size, 16-B units
+};
+
+struct DeviceScene {
+    void *blob = nullptr;
+    int32_t blob_units = 0;
+    int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
+    int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
+};
+
+// rt_kernel.hip
+hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t stream);
+size_t lds_bytes(const LaunchParams &p);
+
+// rt_api.cpp
+void set_error(const std::string &msg);
+
+}  // namespace rtamd
+
+struct rt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float4 *staging = nullptr;  // device buffer for host-destination renders
+    size_t staging_px = 0;
+    bool timed = false;
+};
+
+struct rt_scene {
+    int device = 0;
+    rtamd::DeviceScene dev;
+};

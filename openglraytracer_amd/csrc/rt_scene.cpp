@@ -1,0 +1,368 @@
+// rt_scene.cpp — host side of the hot path: the reference scene / camera
+// restated as C++ data, the frame constants (camera unprojection, per-object
+// transforms) and the device-resident scene blob.
+//
+// Frame constants are evaluated in float64 and rounded once to float32. The
+// reference evaluates them in float32 per ray (raytrace_compute.glsl:366-383,
+// :650-652, :718); the unprojection inverse(proj*view) is ill-conditioned
+// (near/far = 1e-4) and llvmpipe's float result depends on how its compiler
+// re-associates inexact float ops, so no float order reproduces it — float64
+// is the closest independent estimate ("Parity").
+// Everything the kernel evaluates per pixel stays float32 in GLSL order.
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "rt_internal.h"
+
+using namespace rtamd;
+
+namespace {
+
+constexpr float kPi = 3.14159265358f;            // raytrace_compute.glsl:13
+constexpr float kDegToRad = kPi / 180.0f;         // :17 (folded in float)
+
+struct M4 {
+    double m[4][4];  // column-major, m[col][row] as GLSL
+};
+
+M4 ident() {
+    M4 r{};
+    for (int i = 0; i < 4; ++i) r.m[i][i] = 1.0;
+    return r;
+}
+
+M4 mul(const M4 &a, const M4 &b) {
+    M4 r{};
+    for (int c = 0; c < 4; ++c)
+        for (int row = 0; row < 4; ++row) {
+            double acc = 0.0;
+            for (int k = 0; k < 4; ++k) acc += a.m[k][row] * b.m[c][k];
+            r.m[c][row] = acc;
+        }
+    return r;
+}
+
+// Inverse via the 4x4 adjugate (float64).
+M4 inverse(const M4 &a) {
+    const double *s = &a.m[0][0];  // column-major linear
+    double inv[16];
+    inv[0] = s[5] * s[10] * s[15] - s[5] * s[11] * s[14] - s[9] * s[6] * s[15] + s[9] * s[7] * s[14] +
+             s[13] * s[6] * s[11] - s[13] * s[7] * s[10];
+    inv[4] = -s[4] * s[10] * s[15] + s[4] * s[11] * s[14] + s[8] * s[6] * s[15] - s[8] * s[7] * s[14] -
+             s[12] * s[6] * s[11] + s[12] * s[7] * s[10];
+    inv[8] = s[4] * s[9] * s[15] - s[4] * s[11] * s[13] - s[8] * s[5] * s[15] + s[8] * s[7] * s[13] +
+             s[12] * s[5] * s[11] - s[12] * s[7] * s[9];
+    inv[12] = -s[4] * s[9] * s[14] + s[4] * s[10] * s[13] + s[8] * s[5] * s[14] - s[8] * s[6] * s[13] -
+              s[12] * s[5] * s[10] + s[12] * s[6] * s[9];
+    inv[1] = -s[1] * s[10] * s[15] + s[1] * s[11] * s[14] + s[9] * s[2] * s[15] - s[9] * s[3] * s[14] -
+             s[13] * s[2] * s[11] + s[13] * s[3] * s[10];
+    inv[5] = s[0] * s[10] * s[15] - s[0] * s[11] * s[14] - s[8] * s[2] * s[15] + s[8] * s[3] * s[14] +
+             s[12] * s[2] * s[11] - s[12] * s[3] * s[10];
+    inv[9] = -s[0] * s[9] * s[15] + s[0] * s[11] * s[13] + s[8] * s[1] * s[15] - s[8] * s[3] * s[13] -
+             s[12] * s[1] * s[11] + s[12] * s[3] * s[9];
+    inv[13] = s[0] * s[9] * s[14] - s[0] * s[10] * s[13] - s[8] * s[1] * s[14] + s[8] * s[2] * s[13] +
+              s[12] * s[1] * s[10] - s[12] * s[2] * s[9];
+    inv[2] = s[1] * s[6] * s[15] - s[1] * s[7] * s[14] - s[5] * s[2] * s[15] + s[5] * s[3] * s[14] +
+             s[13] * s[2] * s[7] - s[13] * s[3] * s[6];
+    inv[6] = -s[0] * s[6] * s[15] + s[0] * s[7] * s[14] + s[4] * s[2] * s[15] - s[4] * s[3] * s[14] -
+             s[12] * s[2] * s[7] + s[12] * s[3] * s[6];
+    inv[10] = s[0] * s[5] * s[15] - s[0] * s[7] * s[13] - s[4] * s[1] * s[15] + s[4] * s[3] * s[13] +
+              s[12] * s[1] * s[7] - s[12] * s[3] * s[5];
+    inv[14] = -s[0] * s[5] * s[14] + s[0] * s[6] * s[13] + s[4] * s[1] * s[14] - s[4] * s[2] * s[13] -
+              s[12] * s[1] * s[6] + s[12] * s[2] * s[5];
+    inv[3] = -s[1] * s[6] * s[11] + s[1] * s[7] * s[10] + s[5] * s[2] * s[11] - s[5] * s[3] * s[10] -
+             s[9] * s[2] * s[7] + s[9] * s[3] * s[6];
+    inv[7] = s[0] * s[6] * s[11] - s[0] * s[7] * s[10] - s[4] * s[2] * s[11] + s[4] * s[3] * s[10] +
+             s[8] * s[2] * s[7] - s[8] * s[3] * s[6];
+    inv[11] = -s[0] * s[5] * s[11] + s[0] * s[7] * s[9] + s[4] * s[1] * s[11] - s[4] * s[3] * s[9] -
+              s[8] * s[1] * s[7] + s[8] * s[3] * s[5];
+    inv[15] = s[0] * s[5] * s[10] - s[0] * s[6] * s[9] - s[4] * s[1] * s[10] + s[4] * s[2] * s[9] +
+              s[8] * s[1] * s[6] - s[8] * s[2] * s[5];
+    double det = s[0] * inv[0] + s[1] * inv[4] + s[2] * inv[8] + s[3] * inv[12];
+    M4 r;
+    double *o = &r.m[0][0];
+    for (int i = 0; i < 16; ++i) o[i] = inv[i] / det;
+    return r;
+}
+
+// rotation_matrix_{x,y,z} (:444-486): the angle enters as the float
+// DEG_TO_RAD * deg the shader forms, then cos/sin in float64.
+M4 rot(int axis, float deg) {
+    const double a = static_cast<double>(kDegToRad * deg);
+    const double c = std::cos(a), s = std::sin(a);
+    M4 r = ident();
+    if (axis == 0) { r.m[1][1] = c; r.m[1][2] = s; r.m[2][1] = -s; r.m[2][2] = c; }
+    if (axis == 1) { r.m[0][0] = c; r.m[0][2] = -s; r.m[2][0] = s; r.m[2][2] = c; }
+    if (axis == 2) { r.m[0][0] = c; r.m[0][1] = s; r.m[1][0] = -s; r.m[1][1] = c; }
+    return r;
+}
+
+// calc_transform_matrix (:529-532) = translation (:432) * rotation (:492-503:
+// yaw about z, then pitch about x, then roll about y).
+M4 transform(const float pos[3], const float ang[3]) {
+    M4 t = ident();
+    t.m[3][0] = pos[0];
+    t.m[3][1] = pos[1];
+    t.m[3][2] = pos[2];
+    return mul(t, mul(mul(rot(2, ang[1]), rot(0, ang[0])), rot(1, ang[2])));
+}
+
+void set4(float *d, float a, float b, float c, float e) {
+    d[0] = a; d[1] = b; d[2] = c; d[3] = e;
+}
+void set4s(float *d, float s) { set4(d, s, s, s, s); }
+
+void set_material(rt_material &m, float amb, const float dif[4], float spe, float shin, float refl, float transp,
+                  float ior) {
+    set4s(m.ambient, amb);
+    std::memcpy(m.diffuse, dif, 16);
+    set4s(m.specular, spe);
+    m.shininess = shin;
+    set4s(m.emissive, 0.0f);
+    m.reflectivity = refl;
+    m.transparency = transp;
+    m.refraction_index = ior;
+}
+
+void make_object(rt_object &o, float mn[3], float mx[3], float radius, float p0, float p1, float p2, float a0, float a1,
+                 float a2, int mat) {
+    std::memcpy(o.box_mins, mn, 12);
+    std::memcpy(o.box_maxs, mx, 12);
+    o.radius = radius;
+    o.position[0] = p0; o.position[1] = p1; o.position[2] = p2;
+    o.angles[0] = a0; o.angles[1] = a1; o.angles[2] = a2;
+    o.material = mat;
+}
+
+// get_closest_collision's type test (:749-771).
+int object_kind(const rt_object &o) {
+    const bool box = !(o.box_mins[0] == 0.0f && o.box_mins[1] == 0.0f && o.box_mins[2] == 0.0f &&
+                       o.box_maxs[0] == 0.0f && o.box_maxs[1] == 0.0f && o.box_maxs[2] == 0.0f);
+    if (box) return 1;
+    if (o.radius != -1.0f) return 2;
+    return 0;
+}
+
+uint64_t splitmix64(uint64_t &state) {
+    state += 0x9E3779B97F4A7C15ULL;
+    uint64_t z = state;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+float uniform(uint64_t &state, double lo, double hi) {
+    const double u = static_cast<double>(splitmix64(state) >> 11) * (1.0 / 9007199254740992.0);
+    return static_cast<float>(lo + (hi - lo) * u);
+}
+
+}  // namespace
+
+extern "C" {
+
+// raytrace_compute.glsl:74-157
+int rt_reference_materials(rt_material out[RT_REFERENCE_MATERIALS]) {
+    if (!out) { set_error("rt_reference_materials: null out"); return RT_ERR_INVALID; }
+    const float d1[4] = {0.5f, 0.0f, 0.0f, 1.0f}, d2[4] = {0.3f, 0.6f, 0.3f, 1.0f};
+    const float dr[4] = {1, 0, 0, 1}, dg[4] = {0, 1, 0, 1}, db[4] = {0, 0, 1, 1};
+    const float dm[4] = {0.6f, 0.6f, 0.6f, 1.0f}, dw[4] = {0.4f, 0.4f, 0.4f, 0.4f};
+    set_material(out[RT_MAT_MATERIAL1], 1.0f, d1, 1.0f, 4.0f, 1.0f, 0.0f, 1.5f);
+    set_material(out[RT_MAT_MATERIAL2], 1.0f, d2, 1.0f, 4.0f, 1.0f, 0.0f, 1.5f);
+    set_material(out[RT_MAT_RED_GLASS], 1.0f, dr, 1.0f, 10.0f, 0.8f, 0.4f, 1.5f);
+    set_material(out[RT_MAT_GREEN_GLASS], 1.0f, dg, 1.0f, 10.0f, 0.4f, 0.6f, 1.5f);
+    set_material(out[RT_MAT_BLUE_GLASS], 1.0f, db, 1.0f, 10.0f, 0.4f, 0.6f, 1.5f);
+    set_material(out[RT_MAT_MIRROR], 1.0f, dm, 1.0f, 4.0f, 1.0f, 0.0f, 1.0f);
+    set_material(out[RT_MAT_WALL], 0.5f, dw, 0.3f, 3.0f, 0.3f, 0.0f, 1.0f);
+    return RT_OK;
+}
+
+// raytrace_compute.glsl:199-224
+int rt_reference_lights(rt_light out[RT_REFERENCE_LIGHTS]) {
+    if (!out) { set_error("rt_reference_lights: null out"); return RT_ERR_INVALID; }
+    const float pos[3][3] = {{0.1f, 0.1f, 0.1f}, {7.0f, 7.0f, 2.0f}, {3.0f, -3.0f, 4.0f}};
+    for (int i = 0; i < 3; ++i) std::memcpy(out[i].position, pos[i], 12);
+    set4s(out[0].ambient, 0.3f); set4s(out[0].diffuse, 0.0f); set4s(out[0].specular, 0.0f);
+    set4s(out[1].ambient, 0.05f); set4s(out[1].diffuse, 1.0f); set4s(out[1].specular, 1.0f);
+    set4s(out[2].ambient, 0.05f);
+    set4(out[2].diffuse, 1.0f, 0.0f, 0.0f, 1.0f);
+    set4(out[2].specular, 1.0f, 0.0f, 0.0f, 1.0f);
+    return RT_OK;
+}
+
+// raytrace_compute.glsl:236-237 (scaled_time), :261-321 (objects)
+int rt_reference_objects(float time, rt_object out[RT_REFERENCE_OBJECTS]) {
+    if (!out) { set_error("rt_reference_objects: null out"); return RT_ERR_INVALID; }
+    const float st = time * 0.4f;
+    float zero[3] = {0, 0, 0};
+    float mn0[3] = {-11, -11, -11}, mx0[3] = {11, 11, 11};
+    make_object(out[0], mn0, mx0, -1.0f, 0, 0, 0, 0, 0, 0, RT_MAT_WALL);
+    const float s = 0.5f * std::sin(st * 0.5f) + 1.5f;
+    float mn1[3] = {-1.0f * s, -1.0f * s, -1.0f * s}, mx1[3] = {1.0f * s, 1.0f * s, 1.0f * s};
+    make_object(out[1], mn1, mx1, -1.0f, 0, 0, std::sin(st * 3.0f), 0, st * 90.0f, 0, RT_MAT_MIRROR);
+    float mn2[3] = {-10, -10, -1}, mx2[3] = {10, 10, 1};
+    make_object(out[2], mn2, mx2, -1.0f, 0, 0, -3, std::sin(st * 5.0f) * 10.0f, 45.0f, 0, RT_MAT_GREEN_GLASS);
+    float mn3[3] = {-1, -1, -2}, mx3[3] = {1, 1, 2};
+    make_object(out[3], mn3, mx3, -1.0f, 3, 4, 1, 45.0f + st * 45.0f, 0, 45.0f + st * 180.0f, RT_MAT_BLUE_GLASS);
+    make_object(out[4], zero, zero, 2.0f, -3, 4, 1, 0, 0, 0, RT_MAT_RED_GLASS);
+    return RT_OK;
+}
+
+// raytrace_compute.glsl:334-364
+int rt_reference_camera(float time, rt_camera *out) {
+    if (!out) { set_error("rt_reference_camera: null out"); return RT_ERR_INVALID; }
+    const float radius = 10.0f;
+    const float speed = time * 0.4f + 0.5f;
+    out->position[0] = radius * std::cos(speed);
+    out->position[1] = radius * std::sin(speed);
+    out->position[2] = 0.0f;
+    const float x = 1.0f * speed * (180.0f / 3.1416f);
+    const float yaw = (x - 360.0f * std::floor(x / 360.0f)) + 90.0f;  // GLSL mod
+    out->angles[0] = 0.0f;
+    out->angles[1] = yaw;
+    out->angles[2] = 0.0f;
+    out->near_plane = 0.1f;
+    out->far_plane = 1000.0f;
+    out->aspect = 16.0f / 9.0f;
+    out->v_fov = 90.0f;
+    return RT_OK;
+}
+
+int rt_bench_objects(int n_spheres, uint64_t seed, rt_object *out) {
+    if (!out || n_spheres < 0 || n_spheres + 1 > RT_MAX_OBJECTS) {
+        set_error("rt_bench_objects: bad arguments");
+        return RT_ERR_INVALID;
+    }
+    float mn[3] = {-11, -11, -11}, mx[3] = {11, 11, 11}, zero[3] = {0, 0, 0};
+    make_object(out[0], mn, mx, -1.0f, 0, 0, 0, 0, 0, 0, RT_MAT_WALL);
+    static const int cycle[6] = {RT_MAT_MATERIAL1, RT_MAT_MATERIAL2, RT_MAT_RED_GLASS,
+                                 RT_MAT_GREEN_GLASS, RT_MAT_BLUE_GLASS, RT_MAT_MIRROR};
+    uint64_t st = seed;
+    for (int i = 0; i < n_spheres; ++i) {
+        const float cx = uniform(st, -8.0, 8.0);
+        const float cy = uniform(st, -8.0, 8.0);
+        const float cz = uniform(st, -4.0, 4.0);
+        const float r = uniform(st, 0.3, 1.2);
+        make_object(out[i + 1], zero, zero, r, cx, cy, cz, 0, 0, 0, cycle[i % 6]);
+    }
+    return RT_OK;
+}
+
+// main() :366-392 — P (:411-426) and V = inverse(T * R * Rx(90)) (:538-545),
+// unprojection = inverse(P * V), all in float64, rounded once.
+int rt_make_view(const rt_camera *cam_in, float time, rt_view *out) {
+    if (!out) { set_error("rt_make_view: null out"); return RT_ERR_INVALID; }
+    rt_camera cam;
+    if (cam_in) cam = *cam_in;
+    else rt_reference_camera(time, &cam);
+    const double q = 1.0 / std::tan(static_cast<double>(kDegToRad * 0.5f * cam.v_fov));
+    const double n = cam.near_plane, f = cam.far_plane;
+    M4 P{};
+    P.m[0][0] = q / cam.aspect;
+    P.m[1][1] = q;
+    P.m[2][2] = (n + f) / (n - f);
+    P.m[2][3] = -1.0;
+    P.m[3][2] = (2.0 * n * f) / (n - f);
+    const M4 V = inverse(mul(transform(cam.position, cam.angles), rot(0, 90.0f)));
+    const M4 U = inverse(mul(P, V));
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) out->unprojection[c * 4 + r] = static_cast<float>(U.m[c][r]);
+    std::memcpy(out->origin, cam.position, 12);
+    return RT_OK;
+}
+
+}  // extern "C"
+
+namespace rtamd {
+
+// Build the device blob: [spheres][sphere meta][boxes][materials][lights]
+// [light x material products]; every section 16-B aligned.
+int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
+                int n_lights, std::vector<float4> &blob, DeviceScene &ds) {
+    std::vector<SphereRec> sph;
+    std::vector<SphereMeta> smeta;
+    std::vector<BoxRec> boxes;
+    for (int i = 0; i < n_objs; ++i) {
+        const rt_object &o = objs[i];
+        const int kind = object_kind(o);
+        if (kind == 0) continue;
+        if (o.material < 0 || o.material >= n_mats) {
+            set_error("rt_scene_create: object " + std::to_string(i) + " has material index out of range");
+            return RT_ERR_INVALID;
+        }
+        if (kind == 2) {
+            sph.push_back({o.position[0], o.position[1], o.position[2], o.radius * o.radius});
+            smeta.push_back({i, o.material, o.radius, 0});
+        } else {
+            const M4 L = transform(o.position, o.angles);
+            const M4 W = inverse(L);
+            BoxRec b{};
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 4; ++c) {
+                    b.w2l[r * 4 + c] = static_cast<float>(W.m[c][r]);
+                    b.l2w[r * 4 + c] = static_cast<float>(L.m[c][r]);
+                }
+            // transpose(inverse(mat3(L))) = transpose of inverse(L)'s 3x3 block;
+            // stored row-major: nrm[r][c] = inverse(L)[c][r] read transposed.
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) b.nrm[r * 3 + c] = static_cast<float>(W.m[r][c]);
+            std::memcpy(b.mins, o.box_mins, 12);
+            std::memcpy(b.maxs, o.box_maxs, 12);
+            b.obj_index = i;
+            b.material = o.material;
+            boxes.push_back(b);
+        }
+    }
+    std::vector<MatRec> mrec(n_mats);
+    std::vector<LightMatRec> lm(static_cast<size_t>(n_mats) * n_lights);
+    for (int m = 0; m < n_mats; ++m) {
+        MatRec &r = mrec[m];
+        for (int k = 0; k < 4; ++k) {
+            float acc = 0.0f;  // ambient = vec4(0.0); ambient += La * Ma (:793, :801)
+            for (int j = 0; j < n_lights; ++j) acc = acc + lights[j].ambient[k] * mats[m].ambient[k];
+            r.amb_sum[k] = acc;
+            r.emissive[k] = mats[m].emissive[k];
+        }
+        r.shininess = mats[m].shininess;
+        r.reflectivity = mats[m].reflectivity;
+        r.transparency = mats[m].transparency;
+        r.refraction_index = mats[m].refraction_index;
+        for (int j = 0; j < n_lights; ++j)
+            for (int k = 0; k < 4; ++k) {
+                lm[m * n_lights + j].ld_md[k] = lights[j].diffuse[k] * mats[m].diffuse[k];   // :830
+                lm[m * n_lights + j].ls_ms[k] = lights[j].specular[k] * mats[m].specular[k];  // :832
+            }
+    }
+    std::vector<LightRec> lrec(n_lights);
+    for (int j = 0; j < n_lights; ++j) {
+        std::memcpy(lrec[j].pos, lights[j].position, 12);
+        lrec[j].pad = 0.0f;
+    }
+    auto units = [](size_t bytes) { return static_cast<int32_t>((bytes + 15) / 16); };
+    int32_t off = 0;
+    ds.off_spheres = off; off += units(sph.size() * sizeof(SphereRec));
+    ds.off_smeta = off;   off += units(smeta.size() * sizeof(SphereMeta));
+    ds.off_boxes = off;   off += units(boxes.size() * sizeof(BoxRec));
+    ds.off_mats = off;    off += units(mrec.size() * sizeof(MatRec));
+    ds.off_lights = off;  off += units(lrec.size() * sizeof(LightRec));
+    ds.off_lightmat = off; off += units(lm.size() * sizeof(LightMatRec));
+    ds.blob_units = off;
+    ds.n_spheres = static_cast<int32_t>(sph.size());
+    ds.n_boxes = static_cast<int32_t>(boxes.size());
+    ds.n_mats = n_mats;
+    ds.n_lights = n_lights;
+    blob.assign(static_cast<size_t>(off > 0 ? off : 1), float4{0, 0, 0, 0});
+    auto put = [&](int32_t at, const void *src, size_t bytes) {
+        if (bytes) std::memcpy(reinterpret_cast<char *>(blob.data()) + static_cast<size_t>(at) * 16, src, bytes);
+    };
+    put(ds.off_spheres, sph.data(), sph.size() * sizeof(SphereRec));
+    put(ds.off_smeta, smeta.data(), smeta.size() * sizeof(SphereMeta));
+    put(ds.off_boxes, boxes.data(), boxes.size() * sizeof(BoxRec));
+    put(ds.off_mats, mrec.data(), mrec.size() * sizeof(MatRec));
+    put(ds.off_lights, lrec.data(), lrec.size() * sizeof(LightRec));
+    put(ds.off_lightmat, lm.data(), lm.size() * sizeof(LightMatRec));
+    return RT_OK;
+}
+
+}  // namespace rtamd

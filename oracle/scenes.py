@@ -1,0 +1,92 @@
+"""Benchmark scenes of SURVEY.md §8(d), restated in Python (test infrastructure).
+
+The product builds the same scenes in C++ (rt_bench_objects, include/rt.h);
+tests check both agree bit-for-bit. Materials and lights are the reference's
+(raytrace_compute.glsl:74-157, :199-224). Positions are float32.
+
+Random stream: splitmix64 (seeded), u = (x >> 11) * 2**-53, value =
+float32(lo + (hi - lo) * u) evaluated in float64.
+"""
+import numpy as np
+
+from openglraytracer_amd.abi import (BLUE_GLASS, GREEN_GLASS, MATERIAL1, MATERIAL2, MIRROR,
+                                     RED_GLASS, WALL, Object)
+
+_M64 = (1 << 64) - 1
+SPHERE_MATERIAL_CYCLE = [MATERIAL1, MATERIAL2, RED_GLASS, GREEN_GLASS, BLUE_GLASS, MIRROR]
+
+
+class SplitMix64:
+    def __init__(self, seed):
+        self.state = seed & _M64
+
+    def next(self):
+        self.state = (self.state + 0x9E3779B97F4A7C15) & _M64
+        z = self.state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+        return z ^ (z >> 31)
+
+    def uniform(self, lo, hi):
+        u = (self.next() >> 11) * (1.0 / 9007199254740992.0)
+        return float(np.float32(lo + (hi - lo) * u))
+
+
+def box(mins, maxs, pos, angles, material):
+    o = Object()
+    o.box_mins[:] = mins
+    o.box_maxs[:] = maxs
+    o.radius = -1.0
+    o.position[:] = pos
+    o.angles[:] = angles
+    o.material = material
+    return o
+
+
+def sphere(pos, radius, material):
+    o = Object()
+    o.box_mins[:] = (0.0, 0.0, 0.0)
+    o.box_maxs[:] = (0.0, 0.0, 0.0)
+    o.radius = radius
+    o.position[:] = pos
+    o.angles[:] = (0.0, 0.0, 0.0)
+    o.material = material
+    return o
+
+
+def room_box():
+    """raytrace_compute.glsl:264-273: the +-11 room, wall material."""
+    return box((-11.0,) * 3, (11.0,) * 3, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), WALL)
+
+
+def config1_objects():
+    """Config 1: 4 spheres + the reference's floor-slab idiom as the 'plane'
+    (raytrace_compute.glsl:286-297 with angles 0 and the wall material)."""
+    return [sphere((-3.0, 4.0, 1.0), 2.0, RED_GLASS),
+            sphere((3.0, -4.0, 1.0), 1.5, MIRROR),
+            sphere((3.0, 4.0, 0.0), 1.0, MATERIAL2),
+            sphere((-3.0, -4.0, 0.5), 1.5, MATERIAL1),
+            box((-10.0, -10.0, -1.0), (10.0, 10.0, 1.0), (0.0, 0.0, -3.0), (0.0, 0.0, 0.0), WALL)]
+
+
+def bench_objects(n_spheres, seed=0):
+    """Configs 2-5: room box + n seeded spheres (same stream as rt_bench_objects)."""
+    rng = SplitMix64(seed)
+    objs = [room_box()]
+    for i in range(n_spheres):
+        cx = rng.uniform(-8.0, 8.0)
+        cy = rng.uniform(-8.0, 8.0)
+        cz = rng.uniform(-4.0, 4.0)
+        r = rng.uniform(0.3, 1.2)
+        objs.append(sphere((cx, cy, cz), r, SPHERE_MATERIAL_CYCLE[i % 6]))
+    return objs
+
+
+# name -> (objects builder, width, height, max_depth)
+CONFIGS = {
+    "config1": (config1_objects, 256, 256, 1),
+    "config2": (lambda: bench_objects(16), 1920, 1080, 0),
+    "config3": (lambda: bench_objects(64), 3840, 2160, 2),
+    "config4": (lambda: bench_objects(256), 7680, 4320, 4),
+    "config5": (lambda: bench_objects(16), 1920, 1080, 0),
+}
