@@ -1,0 +1,217 @@
+"""Benchmark: primary rays/s of the MI355X ray tracer on BASELINE.json's config.
+
+Workload (BASELINE.json configs[1]): 1920x1080,
+room box + 16 seeded spheres, the reference's 3 lights and 7 materials,
+max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
+
+A step renders N frames of 1920x1080 (N = number of GPUs; frame k is the
+reference orbit camera at time k/60 s). Every frame is row-tiled across the N
+ranks in interleaved 8-row blocks (rt_render_shard); rank 0 assembles the N
+frames with one RCCL gather over xGMI plus a row de-interleave. Per-GPU work
+is one frame per step at every N: weak scaling. At N=1 a step is one full
+frame rendered in place (no collective).
+
+value = primary rays of all frames / step time (max over ranks), Mrays/s.
+roofline = the render kernel against the HBM-write roofline: 16 B per pixel
+(one float4 store) / average kernel time from HIP events on the launch stream.
+cpu_baseline = the reference's own shader on Mesa llvmpipe (oracle/_ref) over a
+bounded band of the same frame, in a child process on the host cores.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+WIDTH, HEIGHT, N_SPHERES, MAX_DEPTH = 1920, 1080, 16, 0
+BLOCK_ROWS = 8
+BYTES_PER_PIXEL = 16  # one float4 store per pixel (algorithmic HBM bytes)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "primary Mrays/s at 1920×1080; achieved HBM GB/s vs peak; 1/2/4/8-GPU scaling"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="approximate budget of the llvmpipe baseline sample")
+    return ap.parse_args()
+
+
+def frame_time(k):
+    return k / 60.0
+
+
+def cpu_baseline(budget_s):
+    """Time the reference shader on llvmpipe (child process) on a band of rows."""
+    threads = min(16, os.cpu_count() or 1)
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), "--threads", str(threads),
+           "--budget", str(budget_s)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=max(120, 6 * budget_s))
+        if r.returncode == 0:
+            return json.loads(r.stdout.strip().splitlines()[-1])
+        sys.stderr.write("cpu baseline failed: %s\n" % r.stderr[-2000:])
+    except Exception as e:  # the baseline is reported, never required
+        sys.stderr.write("cpu baseline failed: %r\n" % (e,))
+    return None
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of the render kernel from the committed PMC pass
+    (profiles/pmc_latest.json, written by tools/pmc_summary.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == "config2" and d.get("n_gpus", 1) == 1:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import openglraytracer_amd as rt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    ctx = rt.Context(local)
+    scene = rt.Scene(ctx, rt.bench_objects(N_SPHERES, 0))
+    n_frames = world
+    views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    if world == 1:
+        frames = torch.empty((1, HEIGHT, WIDTH, 4), dtype=torch.float32, device="cuda")
+        shard_rows = HEIGHT
+    else:
+        shard_rows = max(rt.shard_rows(HEIGHT, BLOCK_ROWS, world, s) for s in range(world))
+        mine = rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
+        shard = torch.zeros((n_frames, shard_rows, WIDTH, 4), dtype=torch.float32, device="cuda")
+        if rank == 0:
+            gathered = [torch.empty_like(shard) for _ in range(world)]
+            frames = torch.empty((n_frames, HEIGHT, WIDTH, 4), dtype=torch.float32, device="cuda")
+            # gathered row (s, i) -> frame row shard_row_ids(s)[i]
+            src, dst = [], []
+            for s in range(world):
+                ids = rt.shard_row_ids(HEIGHT, BLOCK_ROWS, world, s)
+                src.extend(s * shard_rows + np.arange(len(ids)))
+                dst.extend(ids)
+            src_idx = torch.tensor(src, device="cuda")
+            dst_idx = torch.tensor(dst, device="cuda")
+        else:
+            gathered = None
+
+    # HIP events around every render launch of the timed region, on the
+    # stream the kernel is launched on
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(n_frames)] for _ in range(args.steps)]
+
+    def step(timed, it=0):
+        for k in range(n_frames):
+            if timed:
+                ev[it][k][0].record(stream)
+            if world == 1:
+                rt.render_device(ctx, scene, frames[k].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH,
+                                 view=views[k], stream=sh)
+            else:
+                rt.render_shard(ctx, scene, shard[k].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, BLOCK_ROWS,
+                                world, rank, view=views[k], stream=sh)
+            if timed:
+                ev[it][k][1].record(stream)
+        if world > 1:
+            dist.gather(shard, gathered, dst=0)
+            if rank == 0:
+                # (world*shard_rows, n_frames, W, 4): gathered row r of shard s
+                # sits at s*shard_rows + r; de-interleave into frame row order
+                flat = torch.cat([g.transpose(0, 1) for g in gathered], 0)
+                frames.index_copy_(1, dst_idx, flat.index_select(0, src_idx).transpose(0, 1))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(args.steps):
+        step(True, it)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kernel_ms = [a.elapsed_time(b) for row in ev for a, b in row]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    rays = n_frames * WIDTH * HEIGHT * args.steps
+    value = rays / elapsed / 1e6
+    avg_kernel_ms = float(np.mean(kernel_ms))
+    px_per_launch = WIDTH * (HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank))
+    achieved = px_per_launch * BYTES_PER_PIXEL / (avg_kernel_ms * 1e-3) / 1e9
+    traffic = pmc_traffic() if world == 1 else None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded scene, SURVEY.md §8(d) config 2)",
+            "config": {"workload": "config2: 1920x1080, room box + 16 spheres, max_depth 0 "
+                                   "(primary + shadow rays)",
+                       "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES, "max_depth": MAX_DEPTH,
+                       "frames_per_step": n_frames, "row_block": BLOCK_ROWS,
+                       "parallelism": "row-tiles x%d + RCCL gather" % world if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic,
+                         "kernel_ms": round(avg_kernel_ms, 5),
+                         "bytes_per_launch": px_per_launch * BYTES_PER_PIXEL},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    scene.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

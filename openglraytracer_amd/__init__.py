@@ -1,0 +1,240 @@
+"""MI355X-native per-pixel ray tracer — host-side Python front-end of the C-ABI.
+
+The hot path (raytrace_compute.glsl of blubs/OpenGLRaytracer) runs as a HIP
+kernel in libopenglraytracer_amd.so (built in-tree by `make -C
+openglraytracer_amd/csrc`, or __graft_entry__.build()). This module is a thin
+ctypes binding of include/rt.h mirroring the reference's frame driver
+(OpenGLRaytracer/main.cpp:219-238): build a scene, pick `time`, render a
+W x H frame into a float RGBA surface.
+
+There is no CPU fallback: if the library is missing, or no GPU is present,
+every render call raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from .abi import (RT_MAX_DEPTH, RT_OK, Camera, Light, Material, Object)  # noqa: F401
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libopenglraytracer_amd.so")
+_lib = None
+
+
+class RTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("rt error %d: %s" % (code, msg))
+        self.code = code
+
+
+class View(C.Structure):
+    """rt_view: column-major inverse(proj*view) + ray origin (include/rt.h)."""
+    _fields_ = [("unprojection", C.c_float * 16), ("origin", C.c_float * 3)]
+
+
+def lib():
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libopenglraytracer_amd.so not built: run __graft_entry__.build() "
+                               "or `make -C openglraytracer_amd/csrc`")
+        # One HIP runtime per process: PyTorch-ROCm bundles its own
+        # libamdhip64 (loaded by `import torch` under the unversioned name),
+        # while this library links the SONAME libamdhip64.so.7. Importing torch
+        # first lets the dynamic linker bind this library to torch's runtime,
+        # so device pointers, streams and RCCL are shared; the other order
+        # would load two runtimes and torch would find no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = C.CDLL(LIB_PATH)
+        vp, i, f = C.c_void_p, C.c_int, C.c_float
+        sig = {
+            "rt_reference_materials": ([vp], i), "rt_reference_lights": ([vp], i),
+            "rt_reference_objects": ([f, vp], i), "rt_reference_camera": ([f, vp], i),
+            "rt_bench_objects": ([i, C.c_uint64, vp], i), "rt_make_view": ([vp, f, vp], i),
+            "rt_create": ([i, vp], i), "rt_destroy": ([vp], None),
+            "rt_scene_create": ([vp, vp, i, vp, i, vp, i, vp], i), "rt_scene_destroy": ([vp], None),
+            "rt_render": ([vp, vp, vp, f, i, i, i, i, i, vp, i, vp], i),
+            "rt_render_view": ([vp, vp, vp, i, i, i, i, i, vp, i, vp], i),
+            "rt_shard_rows": ([i, i, i, i], i),
+            "rt_render_shard": ([vp, vp, vp, i, i, i, i, i, i, vp, vp], i),
+            "rt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i),
+            "rt_pack_rgba8": ([vp, C.c_size_t, vp], i),
+            "rt_last_error": ([], C.c_char_p), "rt_version": ([], C.c_char_p),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != RT_OK:
+        raise RTError(rc, lib().rt_last_error().decode())
+
+
+# ---- reference scene / camera (raytrace_compute.glsl:74-364) ---------------
+def reference_materials():
+    m = (Material * 7)()
+    _check(lib().rt_reference_materials(m))
+    return list(m)
+
+
+def reference_lights():
+    ls = (Light * 3)()
+    _check(lib().rt_reference_lights(ls))
+    return list(ls)
+
+
+def reference_objects(time=0.0):
+    o = (Object * 5)()
+    _check(lib().rt_reference_objects(time, o))
+    return list(o)
+
+
+def reference_camera(time=0.0):
+    c = Camera()
+    _check(lib().rt_reference_camera(time, C.byref(c)))
+    return c
+
+
+def bench_objects(n_spheres, seed=0):
+    o = (Object * (n_spheres + 1))()
+    _check(lib().rt_bench_objects(n_spheres, seed, o))
+    return list(o)
+
+
+def make_view(camera=None, time=0.0):
+    v = View()
+    _check(lib().rt_make_view(C.byref(camera) if camera is not None else None, time, C.byref(v)))
+    return v
+
+
+def view_from_matrix(unprojection, origin):
+    """An explicit view: 16 column-major floats + 3-float origin."""
+    v = View()
+    v.unprojection[:] = [float(x) for x in np.asarray(unprojection, np.float32).reshape(-1)]
+    v.origin[:] = [float(x) for x in np.asarray(origin, np.float32).reshape(-1)]
+    return v
+
+
+def shard_rows(height, block_rows, n_shards, shard):
+    n = lib().rt_shard_rows(height, block_rows, n_shards, shard)
+    if n < 0:
+        raise RTError(n, "bad shard arguments")
+    return n
+
+
+def shard_row_ids(height, block_rows, n_shards, shard):
+    """Frame rows owned by `shard`, in the order rt_render_shard packs them."""
+    rows = np.arange(height)
+    return rows[(rows // block_rows) % n_shards == shard]
+
+
+def pack_rgba8(rgba):
+    """GL_RGBA8 unorm packing of a float frame (the shipped surface)."""
+    a = np.ascontiguousarray(rgba, np.float32)
+    out = np.zeros(a.shape, np.uint8)
+    _check(lib().rt_pack_rgba8(a.ctypes.data, a.size // 4, out.ctypes.data))
+    return out
+
+
+class Context:
+    """One device (rt_create). Not thread-safe, like a GL context."""
+
+    def __init__(self, device=0):
+        self._h = C.c_void_p()
+        _check(lib().rt_create(device, C.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().rt_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def last_kernel_ms(self):
+        ms = C.c_float()
+        _check(lib().rt_last_kernel_ms(self._h, C.byref(ms)))
+        return ms.value
+
+
+class Scene:
+    """Device-resident scene (rt_scene_create). Defaults: the reference's
+    7 materials and 3 lights."""
+
+    def __init__(self, ctx, objects, materials=None, lights=None):
+        materials = materials if materials is not None else reference_materials()
+        lights = lights if lights is not None else reference_lights()
+        objs = (Object * max(len(objects), 1))(*objects)
+        mats = (Material * len(materials))(*materials)
+        lts = (Light * max(len(lights), 1))(*lights)
+        self._h = C.c_void_p()
+        _check(lib().rt_scene_create(ctx.handle, objs, len(objects), mats, len(materials), lts,
+                                     len(lights), C.byref(self._h)))
+        self.ctx = ctx
+
+    def close(self):
+        if self._h:
+            lib().rt_scene_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+
+def render(ctx, scene, width, height, max_depth=0, time=0.0, camera=None, view=None, rows=None):
+    """Render rows [r0, r1) to a host array (r1-r0, width, 4) float32,
+    synchronously (the reference's glDispatchCompute + glFinish)."""
+    r0, r1 = rows if rows is not None else (0, height)
+    out = np.zeros((r1 - r0, width, 4), np.float32)
+    if view is None:
+        view = make_view(camera, time)
+    _check(lib().rt_render_view(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
+                                r0, r1, out.ctypes.data, 0, None))
+    return out
+
+
+def render_device(ctx, scene, out_ptr, width, height, max_depth=0, view=None, rows=None,
+                  stream=None):
+    """Render into device memory `out_ptr` (e.g. torch tensor.data_ptr()); with
+    `stream` (a hipStream_t as int) the call is asynchronous on that stream."""
+    r0, r1 = rows if rows is not None else (0, height)
+    if view is None:
+        view = make_view(None, 0.0)
+    _check(lib().rt_render_view(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
+                                r0, r1, C.c_void_p(out_ptr), 1,
+                                C.c_void_p(stream) if stream else None))
+
+
+def render_shard(ctx, scene, out_ptr, width, height, max_depth, block_rows, n_shards, shard,
+                 view=None, stream=None):
+    """Render this shard's interleaved row blocks into device memory."""
+    if view is None:
+        view = make_view(None, 0.0)
+    _check(lib().rt_render_shard(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
+                                 block_rows, n_shards, shard, C.c_void_p(out_ptr),
+                                 C.c_void_p(stream) if stream else None))

@@ -1,0 +1,309 @@
+// rt_api.cpp — the C-ABI (include/rt.h): contexts, scenes, render calls.
+//
+// The counterpart of the reference's frame driver (OpenGLRaytracer/main.cpp:
+// 203 program creation, :219-238 draw(): bind image, set `time`,
+// glDispatchCompute(W, H, 1), glFinish). No exception crosses this boundary;
+// failures return RT_ERR_* and leave a thread-local message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rtamd {
+
+namespace {
+thread_local std::string g_error;
+
+int hip_fail(const char *what, hipError_t e) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return RT_ERR_HIP;
+}
+
+// Largest LDS a work-group may request on gfx950 (160 KiB).
+constexpr size_t kMaxLds = 160 * 1024;
+}  // namespace
+
+void set_error(const std::string &msg) { g_error = msg; }
+
+int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
+                int n_lights, std::vector<float4> &blob, DeviceScene &ds);
+hipError_t allow_large_lds(size_t bytes);
+
+}  // namespace rtamd
+
+using namespace rtamd;
+
+namespace {
+
+int check_render_args(const rt_context *ctx, const rt_scene *scene, int width, int height, int max_depth) {
+    if (!ctx || !scene) {
+        set_error("null context or scene");
+        return RT_ERR_INVALID;
+    }
+    if (scene->device != ctx->device) {
+        set_error("scene was created on another device");
+        return RT_ERR_INVALID;
+    }
+    if (width <= 0 || height <= 0 || width > 65536 || height > 65536) {
+        set_error("bad frame size");
+        return RT_ERR_INVALID;
+    }
+    if (max_depth < 0 || max_depth > RT_MAX_DEPTH) {
+        set_error("max_depth " + std::to_string(max_depth) + " outside [0, " + std::to_string(RT_MAX_DEPTH) + "]");
+        return RT_ERR_UNSUPPORTED;
+    }
+    return RT_OK;
+}
+
+LaunchParams base_params(const rt_scene *scene, const rt_view *view, int width, int height) {
+    LaunchParams p{};
+    std::memcpy(p.unproj, view->unprojection, sizeof p.unproj);
+    std::memcpy(p.origin, view->origin, sizeof p.origin);
+    p.width = width;
+    p.height = height;
+    const DeviceScene &d = scene->dev;
+    p.n_spheres = d.n_spheres;
+    p.n_boxes = d.n_boxes;
+    p.n_mats = d.n_mats;
+    p.n_lights = d.n_lights;
+    p.scene = d.blob;
+    p.off_spheres = d.off_spheres;
+    p.off_smeta = d.off_smeta;
+    p.off_boxes = d.off_boxes;
+    p.off_mats = d.off_mats;
+    p.off_lights = d.off_lights;
+    p.off_lightmat = d.off_lightmat;
+    p.blob_units = d.blob_units;
+    return p;
+}
+
+// Launch on `stream` with kernel-time events on the context.
+int launch(rt_context *ctx, const LaunchParams &p, int max_depth, hipStream_t stream) {
+    hipError_t e = hipEventRecord(ctx->ev0, stream);
+    if (e != hipSuccess) return hip_fail("hipEventRecord", e);
+    e = launch_render(p, max_depth, stream);
+    if (e != hipSuccess) return hip_fail("kernel launch", e);
+    e = hipEventRecord(ctx->ev1, stream);
+    if (e != hipSuccess) return hip_fail("hipEventRecord", e);
+    ctx->timed = true;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *rt_last_error(void) { return g_error.c_str(); }
+const char *rt_version(void) { return "openglraytracer_amd 0.1 (gfx950)"; }
+
+int rt_create(int device, rt_context **out) {
+    if (!out) { set_error("rt_create: null out"); return RT_ERR_INVALID; }
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        set_error("rt_create: no HIP device");
+        return RT_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= n) {
+        set_error("rt_create: device " + std::to_string(device) + " out of range");
+        return RT_ERR_NO_DEVICE;
+    }
+    if ((e = hipSetDevice(device)) != hipSuccess) return hip_fail("hipSetDevice", e);
+    rt_context *ctx = new (std::nothrow) rt_context;
+    if (!ctx) { set_error("rt_create: out of memory"); return RT_ERR_NOMEM; }
+    ctx->device = device;
+    if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess ||
+        (e = allow_large_lds(kMaxLds)) != hipSuccess) {
+        rt_destroy(ctx);
+        return hip_fail("rt_create", e);
+    }
+    *out = ctx;
+    return RT_OK;
+}
+
+void rt_destroy(rt_context *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->staging) (void)hipFree(ctx->staging);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt_material *mats, int n_mats,
+                    const rt_light *lights, int n_lights, rt_scene **out) {
+    if (!out) { set_error("rt_scene_create: null out"); return RT_ERR_INVALID; }
+    *out = nullptr;
+    if (!ctx || (n_objs > 0 && !objs) || n_objs < 0 || n_objs > RT_MAX_OBJECTS || !mats || n_mats <= 0 ||
+        n_mats > RT_MAX_MATERIALS || n_lights < 0 || n_lights > RT_MAX_LIGHTS || (n_lights > 0 && !lights)) {
+        set_error("rt_scene_create: bad arguments");
+        return RT_ERR_INVALID;
+    }
+    std::vector<float4> blob;
+    DeviceScene ds;
+    int rc = build_scene(objs, n_objs, mats, n_mats, lights, n_lights, blob, ds);
+    if (rc != RT_OK) return rc;
+    const size_t lds = (static_cast<size_t>(ds.blob_units) + ds.n_spheres + ds.n_boxes) * sizeof(float4);
+    if (lds > kMaxLds) {
+        set_error("rt_scene_create: scene needs " + std::to_string(lds) + " B of LDS (> 160 KiB)");
+        return RT_ERR_UNSUPPORTED;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    e = hipMalloc(&ds.blob, blob.size() * sizeof(float4));
+    if (e != hipSuccess) return hip_fail("hipMalloc(scene)", e);
+    e = hipMemcpy(ds.blob, blob.data(), blob.size() * sizeof(float4), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(ds.blob);
+        return hip_fail("hipMemcpy(scene)", e);
+    }
+    rt_scene *s = new (std::nothrow) rt_scene;
+    if (!s) {
+        (void)hipFree(ds.blob);
+        set_error("rt_scene_create: out of memory");
+        return RT_ERR_NOMEM;
+    }
+    s->device = ctx->device;
+    s->dev = ds;
+    *out = s;
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene *scene) {
+    if (!scene) return;
+    (void)hipSetDevice(scene->device);
+    (void)hipDeviceSynchronize();
+    if (scene->dev.blob) (void)hipFree(scene->dev.blob);
+    delete scene;
+}
+
+int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width, int height, int max_depth,
+                   int row_begin, int row_end, float *out, int out_is_device, void *hip_stream) {
+    int rc = check_render_args(ctx, scene, width, height, max_depth);
+    if (rc != RT_OK) return rc;
+    if (!view || !out || row_begin < 0 || row_end > height || row_begin >= row_end) {
+        set_error("rt_render: bad view / output / row range");
+        return RT_ERR_INVALID;
+    }
+    if (hip_stream && !out_is_device) {
+        set_error("rt_render: an asynchronous render needs a device output buffer");
+        return RT_ERR_INVALID;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    LaunchParams p = base_params(scene, view, width, height);
+    p.row_begin = row_begin;
+    p.n_rows = row_end - row_begin;
+    const size_t n_px = static_cast<size_t>(p.n_rows) * width;
+    hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    if (out_is_device) {
+        p.out = reinterpret_cast<float4 *>(out);
+    } else {
+        if (ctx->staging_px < n_px) {
+            if (ctx->staging) (void)hipFree(ctx->staging);
+            ctx->staging = nullptr;
+            ctx->staging_px = 0;
+            e = hipMalloc(&ctx->staging, n_px * sizeof(float4));
+            if (e != hipSuccess) return hip_fail("hipMalloc(staging)", e);
+            ctx->staging_px = n_px;
+        }
+        p.out = ctx->staging;
+    }
+    rc = launch(ctx, p, max_depth, stream);
+    if (rc != RT_OK) return rc;
+    if (!out_is_device) {
+        e = hipMemcpyAsync(out, ctx->staging, n_px * sizeof(float4), hipMemcpyDeviceToHost, stream);
+        if (e != hipSuccess) return hip_fail("hipMemcpyAsync(out)", e);
+    }
+    if (!hip_stream) {
+        e = hipStreamSynchronize(stream);  // glFinish (main.cpp:238)
+        if (e != hipSuccess) return hip_fail("render", e);
+    }
+    return RT_OK;
+}
+
+int rt_render(rt_context *ctx, const rt_scene *scene, const rt_camera *cam, float time, int width, int height,
+              int max_depth, int row_begin, int row_end, float *out, int out_is_device, void *hip_stream) {
+    rt_view view;
+    int rc = rt_make_view(cam, time, &view);
+    if (rc != RT_OK) return rc;
+    return rt_render_view(ctx, scene, &view, width, height, max_depth, row_begin, row_end, out, out_is_device,
+                          hip_stream);
+}
+
+int rt_shard_rows(int height, int block_rows, int n_shards, int shard) {
+    if (height <= 0 || block_rows <= 0 || n_shards <= 0 || shard < 0 || shard >= n_shards) return RT_ERR_INVALID;
+    const int full = height / block_rows, tail = height % block_rows;
+    int rows = (full / n_shards) * block_rows;
+    const int extra = full % n_shards;  // leftover full blocks go to shards 0..extra-1
+    if (shard < extra) rows += block_rows;
+    if (tail && shard == full % n_shards) rows += tail;
+    return rows;
+}
+
+int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width, int height,
+                    int max_depth, int block_rows, int n_shards, int shard, float *out_device, void *hip_stream) {
+    int rc = check_render_args(ctx, scene, width, height, max_depth);
+    if (rc != RT_OK) return rc;
+    const int rows = rt_shard_rows(height, block_rows, n_shards, shard);
+    if (!view || !out_device || rows < 0) {
+        set_error("rt_render_shard: bad view / output / shard arguments");
+        return RT_ERR_INVALID;
+    }
+    if (rows == 0) return RT_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    LaunchParams p = base_params(scene, view, width, height);
+    p.row_begin = 0;
+    p.n_rows = rows;
+    p.block_rows = block_rows;
+    p.n_shards = n_shards;
+    p.shard = shard;
+    p.out = reinterpret_cast<float4 *>(out_device);
+    hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    rc = launch(ctx, p, max_depth, stream);
+    if (rc != RT_OK) return rc;
+    if (!hip_stream) {
+        e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail("render", e);
+    }
+    return RT_OK;
+}
+
+int rt_last_kernel_ms(rt_context *ctx, float *ms) {
+    if (!ctx || !ms || !ctx->timed) {
+        set_error("rt_last_kernel_ms: nothing timed yet");
+        return RT_ERR_INVALID;
+    }
+    hipError_t e = hipEventSynchronize(ctx->ev1);
+    if (e != hipSuccess) return hip_fail("hipEventSynchronize", e);
+    e = hipEventElapsedTime(ms, ctx->ev0, ctx->ev1);
+    if (e != hipSuccess) return hip_fail("hipEventElapsedTime", e);
+    return RT_OK;
+}
+
+// GL_RGBA8 unorm store of a float colour (main.cpp:152-159, :223): clamp to
+// [0, 1] and round to nearest (alpha stored as written, 0, :404).
+int rt_pack_rgba8(const float *in, size_t n_pixels, uint8_t *out) {
+    if ((!in || !out) && n_pixels) {
+        set_error("rt_pack_rgba8: null buffer");
+        return RT_ERR_INVALID;
+    }
+    for (size_t i = 0; i < n_pixels * 4; ++i) {
+        float v = in[i];
+        v = v != v ? 0.0f : std::min(std::max(v, 0.0f), 1.0f);
+        out[i] = static_cast<uint8_t>(v * 255.0f + 0.5f);
+    }
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -40,8 +40,8 @@ struct BoxRec {
     float maxs[3];
     int32_t obj_index;
     int32_t material;
-    int32_t pad[3];
-};  // 48 floats = 192 B
+    int32_t pad[7];
+};  // 48 words = 192 B
 static_assert(sizeof(BoxRec) == 192, "BoxRec layout");
 
 // Material (:56-69) plus the per-material light products the shading loop
