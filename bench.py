@@ -88,6 +88,7 @@ def main():
     import torch.distributed as dist
 
     import openglraytracer_amd as rt
+    from openglraytracer_amd import frame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -110,21 +111,9 @@ def main():
         shard_rows = HEIGHT
     else:
         shard_rows = max(rt.shard_rows(HEIGHT, BLOCK_ROWS, world, s) for s in range(world))
-        mine = rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
         shard = torch.zeros((n_frames, shard_rows, WIDTH, 4), dtype=torch.float32, device="cuda")
-        if rank == 0:
-            gathered = [torch.empty_like(shard) for _ in range(world)]
-            frames = torch.empty((n_frames, HEIGHT, WIDTH, 4), dtype=torch.float32, device="cuda")
-            # gathered row (s, i) -> frame row shard_row_ids(s)[i]
-            src, dst = [], []
-            for s in range(world):
-                ids = rt.shard_row_ids(HEIGHT, BLOCK_ROWS, world, s)
-                src.extend(s * shard_rows + np.arange(len(ids)))
-                dst.extend(ids)
-            src_idx = torch.tensor(src, device="cuda")
-            dst_idx = torch.tensor(dst, device="cuda")
-        else:
-            gathered = None
+        gathered = [torch.empty_like(shard) for _ in range(world)] if rank == 0 else None
+        frames = None
 
     # HIP events around every render launch of the timed region, on the
     # stream the kernel is launched on
@@ -146,10 +135,7 @@ def main():
         if world > 1:
             dist.gather(shard, gathered, dst=0)
             if rank == 0:
-                # (world*shard_rows, n_frames, W, 4): gathered row r of shard s
-                # sits at s*shard_rows + r; de-interleave into frame row order
-                flat = torch.cat([g.transpose(0, 1) for g in gathered], 0)
-                frames.index_copy_(1, dst_idx, flat.index_select(0, src_idx).transpose(0, 1))
+                frame.assemble(gathered, HEIGHT, BLOCK_ROWS)  # (n_frames, H, W, 4), row order restored
 
     for _ in range(args.warmup):
         step(False)

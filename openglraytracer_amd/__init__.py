@@ -210,12 +210,12 @@ def render(ctx, scene, width, height, max_depth=0, time=0.0, camera=None, view=N
     """Render rows [r0, r1) to a host array (r1-r0, width, 4) float32,
     synchronously (the reference's glDispatchCompute + glFinish)."""
     r0, r1 = rows if rows is not None else (0, height)
-    out = np.zeros((r1 - r0, width, 4), np.float32)
+    out = np.zeros((max(r1 - r0, 1), max(width, 1), 4), np.float32)  # the C-ABI validates the range
     if view is None:
         view = make_view(camera, time)
     _check(lib().rt_render_view(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
                                 r0, r1, out.ctypes.data, 0, None))
-    return out
+    return out[: r1 - r0, :width]
 
 
 def render_device(ctx, scene, out_ptr, width, height, max_depth=0, view=None, rows=None,

@@ -1,0 +1,135 @@
+"""Host side of the drop-in boundary (no GPU needed).
+
+* the C-ABI library loads and exports every entry point include/rt.h declares;
+* the reference scene / camera / benchmark scenes the product builds match the
+  oracle's independent restatement bit-for-bit;
+* frame constants, shard layout, RGBA8 packing and error behaviour.
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import openglraytracer_amd as rt
+from openglraytracer_amd import frame
+from openglraytracer_amd.abi import Light, Material, Object, to_numpy
+from oracle import port, scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "rt.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(rt_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 18
+    lib = rt.lib()
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_every_symbol():
+    import inspect
+    src = inspect.getsource(rt)
+    assert all(s in src for s in declared_symbols())
+
+
+def same(a, b, T):
+    return to_numpy((T * len(a))(*a)).tobytes() == to_numpy((T * len(b))(*b)).tobytes()
+
+
+def test_reference_tables_match_oracle():
+    assert same(rt.reference_materials(), port.reference_materials(), Material)
+    assert same(rt.reference_lights(), port.reference_lights(), Light)
+
+
+@pytest.mark.parametrize("t", [0.0, 0.016, 3.7, 11.25, 123.456])
+def test_reference_objects_and_camera_match_oracle(t):
+    assert same(rt.reference_objects(t), port.reference_objects(t), Object)
+    a, b = rt.reference_camera(t), port.reference_camera(t)
+    assert bytes(memoryview(a)) == bytes(memoryview(b))
+
+
+@pytest.mark.parametrize("n,seed", [(0, 0), (16, 0), (64, 0), (256, 0), (16, 7)])
+def test_bench_scenes_match_oracle(n, seed):
+    assert same(rt.bench_objects(n, seed), scenes.bench_objects(n, seed), Object)
+
+
+def test_make_view_matches_oracle_camera():
+    for t in [0.0, 3.7]:
+        v = rt.make_view(None, t)
+        m = np.zeros(48, np.float32)
+        port.lib().oracle_camera_matrices(None, C.c_float(t), m.ctypes.data_as(C.c_void_p))
+        # the oracle's float32 GLSL-order matrices are within a few ulp-scaled
+        # units of the float64 product (ill-conditioned unprojection)
+        assert np.allclose(np.array(v.unprojection[:]), m[:16], rtol=1e-4, atol=1e-6)
+        cam = rt.reference_camera(t)
+        assert list(v.origin) == list(cam.position)
+
+
+@pytest.mark.parametrize("h", [1, 7, 8, 9, 17, 1080, 4320])
+@pytest.mark.parametrize("b", [1, 8, 16])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_shard_rows_partition_the_frame(h, b, n):
+    ids = [frame.shard_row_ids(h, b, n, s) for s in range(n)]
+    assert sorted(np.concatenate(ids).tolist()) == list(range(h))
+    assert [len(i) for i in ids] == [rt.shard_rows(h, b, n, s) for s in range(n)]
+
+
+def test_assemble_restores_row_order():
+    h, w, b, n = 37, 5, 4, 3
+    full = np.random.default_rng(0).random((2, h, w, 4)).astype(np.float32)
+    pad = frame.padded_shard_rows(h, b, n)
+    shards = []
+    for s in range(n):
+        ids = frame.shard_row_ids(h, b, n, s)
+        x = np.zeros((2, pad, w, 4), np.float32)
+        x[:, :len(ids)] = full[:, ids]
+        shards.append(x)
+    assert np.array_equal(frame.assemble(shards, h, b), full)
+
+
+def test_pack_rgba8_matches_gl_unorm():
+    # (0,0) of the shipped frame reads back from the RGBA8
+    # surface as (0.6666667, 1.0, 0.6392157) = (170, 255, 163)/255
+    px = np.array([[0.6670141, 1.4770919, 0.6400700, 0.0], [-1.0, 0.5, np.nan, 2.0]], np.float32)
+    out = rt.pack_rgba8(px)
+    assert out[0].tolist() == [170, 255, 163, 0]
+    assert out[1].tolist() == [0, 128, 0, 255]
+
+
+def test_errors_without_gpu_are_reported_not_raised_natively():
+    lib = rt.lib()
+    h = C.c_void_p()
+    rc = lib.rt_scene_create(None, None, 0, None, 0, None, 0, C.byref(h))
+    assert rc == rt.abi.RT_ERR_INVALID and b"bad arguments" in lib.rt_last_error()
+    assert lib.rt_shard_rows(10, 0, 2, 0) == rt.abi.RT_ERR_INVALID
+    assert lib.rt_render(None, None, None, 0.0, 8, 8, 0, 0, 8, None, 0, None) == rt.abi.RT_ERR_INVALID
+    assert lib.rt_make_view(None, 0.0, None) == rt.abi.RT_ERR_INVALID
+    assert lib.rt_bench_objects(-1, 0, None) == rt.abi.RT_ERR_INVALID
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(rt.RTError) as e:
+        rt.Context(0)
+    assert e.value.code == rt.abi.RT_ERR_NO_DEVICE
+
+
+def test_product_does_not_import_the_oracle():
+    pkg = os.path.join(ROOT, "openglraytracer_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".cpp", ".hip", ".h")):
+                with open(os.path.join(dirpath, fn)) as f:
+                    text = f.read()
+                assert "oracle" not in re.sub(r"(#|//).*", "", text).lower().replace(
+                    "oracle/rt_oracle.c", ""), fn
