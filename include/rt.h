@@ -173,6 +173,12 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
                     int height, int max_depth, int block_rows, int n_shards, int shard,
                     float *out_device, void *hip_stream);
 
+/* Context options. RT_OPT_CULLING (default 1): skip spheres that provably
+ * cannot be hit (conservative footprints / light cones with margins far
+ * above float error) — output is bit-identical either way. */
+#define RT_OPT_CULLING 1
+int rt_context_set(rt_context *ctx, int option, int value);
+
 /* Kernel-only timing of the last rt_render/rt_render_shard on the context's
  * stream (ms, from HIP events around the launch). */
 int rt_last_kernel_ms(rt_context *ctx, float *ms);

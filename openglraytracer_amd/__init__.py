@@ -64,6 +64,7 @@ def lib():
             "rt_shard_rows": ([i, i, i, i], i),
             "rt_render_shard": ([vp, vp, vp, i, i, i, i, i, i, vp, vp], i),
             "rt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i),
+            "rt_context_set": ([vp, i, i], i),
             "rt_pack_rgba8": ([vp, C.c_size_t, vp], i),
             "rt_last_error": ([], C.c_char_p), "rt_version": ([], C.c_char_p),
         }
@@ -168,6 +169,10 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_culling(self, on):
+        """RT_OPT_CULLING: conservative sphere culling (output identical)."""
+        _check(lib().rt_context_set(self._h, abi.RT_OPT_CULLING, 1 if on else 0))
 
     def last_kernel_ms(self):
         ms = C.c_float()

@@ -33,6 +33,7 @@ void set_error(const std::string &msg) { g_error = msg; }
 int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
                 int n_lights, std::vector<float4> &blob, DeviceScene &ds);
 hipError_t allow_large_lds(size_t bytes);
+bool view_projection(const rt_view &v, float proj[16]);
 
 }  // namespace rtamd
 
@@ -60,8 +61,10 @@ int check_render_args(const rt_context *ctx, const rt_scene *scene, int width, i
     return RT_OK;
 }
 
-LaunchParams base_params(const rt_scene *scene, const rt_view *view, int width, int height) {
+LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_view *view, int width,
+                         int height) {
     LaunchParams p{};
+    p.cull = (view_projection(*view, p.proj) && ctx->culling) ? 1 : 0;
     std::memcpy(p.unproj, view->unprojection, sizeof p.unproj);
     std::memcpy(p.origin, view->origin, sizeof p.origin);
     p.width = width;
@@ -152,7 +155,11 @@ int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt
     DeviceScene ds;
     int rc = build_scene(objs, n_objs, mats, n_mats, lights, n_lights, blob, ds);
     if (rc != RT_OK) return rc;
-    const size_t lds = (static_cast<size_t>(ds.blob_units) + ds.n_spheres + ds.n_boxes) * sizeof(float4);
+    LaunchParams probe{};
+    probe.blob_units = ds.blob_units;
+    probe.n_spheres = ds.n_spheres;
+    probe.n_boxes = ds.n_boxes;
+    const size_t lds = lds_bytes(probe);
     if (lds > kMaxLds) {
         set_error("rt_scene_create: scene needs " + std::to_string(lds) + " B of LDS (> 160 KiB)");
         return RT_ERR_UNSUPPORTED;
@@ -200,7 +207,7 @@ int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, 
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail("hipSetDevice", e);
-    LaunchParams p = base_params(scene, view, width, height);
+    LaunchParams p = base_params(ctx, scene, view, width, height);
     p.row_begin = row_begin;
     p.n_rows = row_end - row_begin;
     const size_t n_px = static_cast<size_t>(p.n_rows) * width;
@@ -262,7 +269,7 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
     if (rows == 0) return RT_OK;
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail("hipSetDevice", e);
-    LaunchParams p = base_params(scene, view, width, height);
+    LaunchParams p = base_params(ctx, scene, view, width, height);
     p.row_begin = 0;
     p.n_rows = rows;
     p.block_rows = block_rows;
@@ -277,6 +284,14 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
         if (e != hipSuccess) return hip_fail("render", e);
     }
     return RT_OK;
+}
+
+int rt_context_set(rt_context *ctx, int option, int value) {
+    if (!ctx) { set_error("rt_context_set: null context"); return RT_ERR_INVALID; }
+    switch (option) {
+        case RT_OPT_CULLING: ctx->culling = value ? 1 : 0; return RT_OK;
+        default: set_error("rt_context_set: unknown option " + std::to_string(option)); return RT_ERR_INVALID;
+    }
 }
 
 int rt_last_kernel_ms(rt_context *ctx, float *ms) {

@@ -40,7 +40,8 @@ struct BoxRec {
     float maxs[3];
     int32_t obj_index;
     int32_t material;
-    int32_t pad[7];
+    uint32_t light_inside;  // bit j: light j strictly inside the box with margin (shadow shortcut)
+    int32_t pad[6];
 };  // 48 words = 192 B
 static_assert(sizeof(BoxRec) == 192, "BoxRec layout");
 
@@ -58,7 +59,7 @@ struct LightMatRec {
 };  // 32 B
 struct LightRec {
     float pos[3];
-    float pad;
+    float dead;  // 1: zero diffuse and specular for every material (no direct term, no shadow ray)
 };
 
 // Per-launch parameters (kernarg, read through the scalar cache).
@@ -73,6 +74,8 @@ struct LaunchParams {
     float4 *out;        // n_rows * width float4
     int32_t off_spheres, off_smeta, off_boxes, off_mats, off_lights, off_lightmat;  // 16-B units
     int32_t blob_units;                                                         // blob size, 16-B units
+    float proj[16];  // column-major proj*view = inverse(unproj) (float64 on the host), for culling
+    int32_t cull;    // 1: exactness-preserving culling enabled (consistent pinhole view)
 };
 
 struct DeviceScene {
@@ -98,6 +101,7 @@ struct rt_context {
     float4 *staging = nullptr;  // device buffer for host-destination renders
     size_t staging_px = 0;
     bool timed = false;
+    int culling = 1;  // RT_OPT_CULLING
 };
 
 struct rt_scene {

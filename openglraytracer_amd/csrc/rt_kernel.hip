@@ -3,12 +3,11 @@
 // One ray per lane; a 256-thread work-group renders a 16x16 pixel tile as
 // four wave64s of 8x8 pixels each (square wave footprints keep the lanes of a
 // wave coherent: they hit the same objects, take the same shading branches and
-// tend to exit the shadow loops together). The whole scene (spheres, boxes,
-// materials, lights) is staged into LDS once per work-group; every lane then
-// reads object records as LDS broadcasts. The frame constants for the camera
-// origin (sphere offset / qc terms, box-local camera position) are computed
-// once per work-group during staging. Each lane ends with one float4 store:
-// a wave writes eight fully-used 128-B lines.
+// cull the same spheres). The whole scene (spheres, boxes, materials, lights)
+// is staged into LDS once per work-group, together with per-frame constants
+// computed there once: the camera-origin terms of every sphere / box and every
+// sphere's conservative screen-space footprint. Each lane ends with one float4
+// store: a wave writes eight fully-used 128-B lines.
 //
 // Arithmetic: float32, GLSL operation order, compiled with -ffp-contract=off
 // and IEEE division / sqrt so every per-pixel value matches the reference's
@@ -22,7 +21,16 @@
 //    finds the closest hit and then tests t < 1, :813-816);
 //  * a light whose unshadowed diffuse+specular contribution leaves the sums
 //    bit-identical (e.g. a light with no diffuse/specular colour, or a
-//    surface facing away) casts no shadow ray — lit and shadowed agree.
+//    surface facing away) casts no shadow ray — lit and shadowed agree;
+//  * culling (conservative, with margins far above float error): a primary
+//    ray skips spheres whose projected footprint misses its wave's 8x8 tile;
+//    a shadow ray skips spheres outside its wave's cone from the light;
+//  * a box whose interior holds the ray origin needs only its three exit
+//    distances (the slab test's t_far), and a shadow ray compares them with 1
+//    without dividing unless the comparison is within 2^-16 of 1.
+// Control flow at function level is wave-uniform (per-lane `valid` masks
+// instead of early returns), so the ballot-based culling always sees all 64
+// lanes; divergence is confined to the innermost exact tests.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -43,6 +51,7 @@ __device__ __forceinline__ v3 mk(float x, float y, float z) { return {x, y, z}; 
 __device__ __forceinline__ v3 add(v3 a, v3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
 __device__ __forceinline__ v3 sub(v3 a, v3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ v3 muls(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ v3 sel(bool c, v3 a, v3 b) { return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z}; }
 // dot(vec3) as llvmpipe associates it: x + (y + z)
 __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
 // normalize(v) = v * inversesqrt(dot(v, v)), inversesqrt = 1 / sqrt (IEEE)
@@ -100,29 +109,57 @@ __device__ __forceinline__ float glsl_exp2(float x) {
 }
 __device__ __forceinline__ float glsl_pow(float x, float y) { return glsl_exp2(glsl_log2(x) * y); }
 
+// ---- wave-wide reductions (called with all 64 lanes active) -------------
+// DPP butterfly within each 16-lane row, then row broadcasts; lane 63 holds
+// the result, read back as a wave-uniform value.
+template <bool kMax>
+__device__ __forceinline__ float dpp_step(float v, float t) { return kMax ? fmaxf(v, t) : fminf(v, t); }
+template <int kCtrl, int kRows>
+__device__ __forceinline__ float dpp(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), kCtrl, kRows, 0xF, false));
+}
+template <bool kMax>
+__device__ __forceinline__ float wave_minmax(float v) {
+    v = dpp_step<kMax>(v, dpp<0xB1, 0xF>(v));   // quad_perm [1,0,3,2]
+    v = dpp_step<kMax>(v, dpp<0x4E, 0xF>(v));   // quad_perm [2,3,0,1]
+    v = dpp_step<kMax>(v, dpp<0x141, 0xF>(v));  // row_half_mirror
+    v = dpp_step<kMax>(v, dpp<0x140, 0xF>(v));  // row_mirror
+    v = dpp_step<kMax>(v, dpp<0x142, 0xA>(v));  // row_bcast:15 into rows 1, 3
+    v = dpp_step<kMax>(v, dpp<0x143, 0xC>(v));  // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_min(float v) { return wave_minmax<false>(v); }
+__device__ __forceinline__ float wave_max(float v) { return wave_minmax<true>(v); }
+__device__ __forceinline__ float lane_value(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
 struct Ray {
     v3 start, dir;
 };
 
 // LDS-resident scene view.
 struct Scene {
-    const float4 *sph;         // cx, cy, cz, r*r
-    const int4 *smeta;         // obj_index, material, radius bits, 0
-    const float4 *sph_cam;     // camera-origin terms: oc = origin - centre, qc (:587-588)
+    const float4 *sph;      // cx, cy, cz, r*r
+    const int4 *smeta;      // obj_index, material, radius bits, 0
+    const float4 *sph_cam;  // camera-origin terms: oc = origin - centre, qc (:587-588)
+    const int4 *sph_px;     // conservative pixel footprint x0, x1, y0, y1 (culling)
     const BoxRec *box;
-    const float4 *box_cam;     // box-local camera origin (:655 for the primary ray)
+    const float4 *box_cam;  // box-local camera origin (:655), w = origin strictly inside
     const MatRec *mat;
     const LightRec *light;
     const LightMatRec *lm;
-    int ns, nb, nl;
+    int ns, nb, nl, nm;
+    int cull;
+    int tx0, tx1, ty0, ty1;  // this wave's pixel rectangle (frame coordinates)
 };
 
 // Hit = the closest object so far: t and reference object index (tie-break).
 struct Hit {
     float t;
-    int obj;     // reference index, -1 = none
-    int slot;    // sphere slot (>= 0) or ~box slot (< 0)
-    bool inside; // sphere: t_near < 0 (:621)
+    int obj;      // reference index, -1 = none
+    int slot;     // sphere slot (>= 0) or ~box slot (< 0)
+    bool inside;  // sphere: t_near < 0 (:621)
 };
 
 __device__ __forceinline__ bool closer(float t, int obj, const Hit &h) {
@@ -132,7 +169,7 @@ __device__ __forceinline__ bool closer(float t, int obj, const Hit &h) {
     return t > 0.0f && (t < h.t || (t == h.t && h.obj >= 0 && obj < h.obj));
 }
 
-// Box slab test (:655-666): local ray, t1 = min(tmin, tmax), t2 = max(...).
+// ---- boxes (:647-724) ----------------------------------------------------
 struct Slab {
     v3 rs, rd, t1, t2;
     float t_near, t_far;
@@ -164,7 +201,60 @@ __device__ __forceinline__ float slab_t(const Slab &s) {
     if (s.t_near >= s.t_far || s.t_far <= 0.0f) return -1.0f;
     return s.t_near < 0.0f ? s.t_far : s.t_near;
 }
+// Origin strictly inside the box on every axis (local coordinates).
+__device__ __forceinline__ bool strictly_inside(const BoxRec &b, v3 rs) {
+    return b.mins[0] < rs.x && rs.x < b.maxs[0] && b.mins[1] < rs.y && rs.y < b.maxs[1] && b.mins[2] < rs.z &&
+           rs.z < b.maxs[2];
+}
+__device__ __forceinline__ bool not_nan(v3 v) { return v.x == v.x && v.y == v.y && v.z == v.z; }
+// Inside the box the slab's t2 on an axis is the exit boundary chosen by the
+// sign of the direction: max((mins-s)/d, (maxs-s)/d) with one division. For
+// d = +-0 the sign bit picks the +inf quotient, exactly as max() does.
+__device__ __forceinline__ float exit_num(float mn, float mx, float s, float d) {
+    return (__float_as_uint(d) >> 31) ? (mn - s) : (mx - s);
+}
+__device__ __forceinline__ v3 exits(const BoxRec &b, v3 rs, v3 rd) {
+    return mk(exit_num(b.mins[0], b.maxs[0], rs.x, rd.x) / rd.x, exit_num(b.mins[1], b.maxs[1], rs.y, rd.y) / rd.y,
+              exit_num(b.mins[2], b.maxs[2], rs.z, rd.z) / rd.z);
+}
+// Box t for the closest-hit loop. With the origin strictly inside and no NaN
+// in the direction: t_near < 0 < t_far, so t = t_far (:690-696).
+__device__ __forceinline__ float box_t(const BoxRec &b, v3 rs, v3 rd, bool inside) {
+    if (inside && not_nan(rd)) {
+        const v3 e = exits(b, rs, rd);
+        return gmin(gmin(e.x, e.y), e.z);
+    }
+    return slab_t(slab(b, rs, rd));
+}
+// fl(num / d) < 1 for a non-negative quotient, dividing only when |num| is
+// within 2^-16 of |d| (correctly rounded division is monotonic).
+__device__ __forceinline__ bool quotient_below_one(float num, float d) {
+    const float an = fabsf(num), ad = fabsf(d);
+    if (an > 1e-30f && ad > 1e-30f) {
+        if (an > ad * 1.0000153f) return false;
+        if (an < ad * 0.9999847f) return true;
+    }
+    return num / d < 1.0f;
+}
+// Does the box hold an occluder with 0 < t < 1 (:813-816)? light_bit: the
+// light is inside the box with a margin (host, float64), so a segment that
+// starts inside ends inside too and exits past t = 1.
+__device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, uint32_t light_bit) {
+    const v3 rs = xform_point(b.w2l, start);
+    const bool inside = strictly_inside(b, rs);
+    if (inside && (b.light_inside & light_bit)) return false;
+    const v3 rd = xform_dir(b.w2l, dir);
+    if (inside && not_nan(rd)) {
+        // t = t_far > 0; occluded iff some exit distance is below 1
+        return quotient_below_one(exit_num(b.mins[0], b.maxs[0], rs.x, rd.x), rd.x) ||
+               quotient_below_one(exit_num(b.mins[1], b.maxs[1], rs.y, rd.y), rd.y) ||
+               quotient_below_one(exit_num(b.mins[2], b.maxs[2], rs.z, rd.z), rd.z);
+    }
+    const float t = slab_t(slab(b, rs, rd));
+    return t > 0.0f && t < 1.0f;
+}
 
+// ---- spheres (:583-640) --------------------------------------------------
 // intersect_sphere_object's t (:586-625) from the ray-invariant terms.
 __device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float qa4, bool &inside) {
     const float qd = qb * qb - qa4 * qc;
@@ -178,62 +268,88 @@ __device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float q
     return inside ? tf : tn;
 }
 
+__device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 d2, float qa2, float qa4,
+                                            bool primary, Hit &h) {
+    float qb, qc;
+    if (primary) {
+        const float4 c = S.sph_cam[s];
+        qb = dot(d2, mk(c.x, c.y, c.z));
+        qc = c.w;
+    } else {
+        const float4 c = S.sph[s];
+        const v3 oc = sub(start, mk(c.x, c.y, c.z));
+        qb = dot(d2, oc);
+        qc = dot(oc, oc) - c.w;
+    }
+    const float qd = qb * qb - qa4 * qc;
+    if (qd >= 0.0f) {  // rare per sphere: keep the divisions off the common path
+        bool inside = false;
+        const float t = sphere_t(qb, qc, qa2, qa4, inside);
+        const int obj = S.smeta[s].x;
+        if (closer(t, obj, h)) h = {t, obj, s, inside};
+    }
+}
+
+// get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r) {
+__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
     Hit h{10000.0f, -1, 0, false};
     for (int b = 0; b < S.nb; ++b) {
         const BoxRec &B = S.box[b];
         v3 rs;
+        bool inside;
         if (kPrimary) {
             const float4 c = S.box_cam[b];
             rs = mk(c.x, c.y, c.z);
+            inside = c.w != 0.0f;
         } else {
             rs = xform_point(B.w2l, r.start);
+            inside = strictly_inside(B, rs);
         }
-        const float t = slab_t(slab(B, rs, xform_dir(B.w2l, r.dir)));
+        const float t = box_t(B, rs, xform_dir(B.w2l, r.dir), inside);
         if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, false};
     }
     const v3 d2 = muls(r.dir, 2.0f);
     const float qa = dot(r.dir, r.dir);
     const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
-    for (int s = 0; s < S.ns; ++s) {
-        float qb, qc;
-        if (kPrimary) {
-            const float4 c = S.sph_cam[s];
-            qb = dot(d2, mk(c.x, c.y, c.z));
-            qc = c.w;
-        } else {
-            const float4 c = S.sph[s];
-            const v3 oc = sub(r.start, mk(c.x, c.y, c.z));
-            qb = dot(d2, oc);
-            qc = dot(oc, oc) - c.w;
+    if (kPrimary && S.cull) {
+        // spheres whose conservative footprint overlaps this wave's tile
+        const int lane = threadIdx.x & 63;
+        for (int base = 0; base < S.ns; base += 64) {
+            const int k = base + lane;
+            bool cand = false;
+            if (k < S.ns) {
+                const int4 bb = S.sph_px[k];
+                cand = !(bb.y < S.tx0 || bb.x > S.tx1 || bb.w < S.ty0 || bb.z > S.ty1);
+            }
+            uint64_t mask = __ballot(cand);
+            while (mask) {
+                const int s = base + __builtin_ctzll(mask);
+                mask &= mask - 1;
+                test_sphere(S, s, r.start, d2, qa2, qa4, true, h);
+            }
         }
-        const float qd = qb * qb - qa4 * qc;
-        if (qd >= 0.0f) {  // rare per sphere: keep the divisions off the common path
-            bool inside = false;
-            const float t = sphere_t(qb, qc, qa2, qa4, inside);
-            const int obj = S.smeta[s].x;
-            if (closer(t, obj, h)) h = {t, obj, s, inside};
-        }
+    } else {
+        for (int s = 0; s < S.ns; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, kPrimary, h);
     }
+    if (!valid) h.obj = -1;
     return h;
 }
 
-// Shadow query (:807-819): is there any object with 0 < t < 1 along
-// start + t * dir? (equivalent to closest-hit t < 1.)
-__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir) {
+// Shadow query (:807-819) for the lanes with `need`: is there an object with
+// 0 < t < 1 along start + t * dir? (equivalent to the closest hit's t < 1).
+// p = the shaded point, L = the light. Called with all lanes active.
+__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, bool need) {
     bool hit = false;
-    for (int b = 0; b < S.nb && !hit; ++b) {
-        const BoxRec &B = S.box[b];
-        const float t = slab_t(slab(B, xform_point(B.w2l, start), xform_dir(B.w2l, dir)));
-        hit = t > 0.0f && t < 1.0f;
-    }
+    const uint32_t light_bit = light < 32 ? 1u << light : 0u;
+    for (int b = 0; b < S.nb; ++b)
+        if (need && !hit) hit = box_occludes(S.box[b], start, dir, light_bit);
+    if (!__any(need && !hit)) return hit;
     const v3 d2 = muls(dir, 2.0f);
     const float qa = dot(dir, dir);
     const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
-    for (int s = 0; s < S.ns; ++s) {
-        if (__all(hit)) break;  // wave-uniform exit once every lane is decided
-        if (!hit) {
+    auto exact = [&](int s) {
+        if (need && !hit) {
             const float4 c = S.sph[s];
             const v3 oc = sub(start, mk(c.x, c.y, c.z));
             const float qb = dot(d2, oc);
@@ -244,6 +360,59 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir) {
                 const float t = sphere_t(qb, qc, qa2, qa4, inside);
                 hit = t > 0.0f && t < 1.0f;
             }
+        }
+    };
+    if (!S.cull) {
+        for (int s = 0; s < S.ns; ++s) {
+            if (!__any(need && !hit)) break;
+            exact(s);
+        }
+        return hit;
+    }
+    // The wave's shadow segments lie within 0.01 (the start offset, :808) of
+    // the segments [L, p_i]: all inside the cone from L with axis `ax` and
+    // half-angle acos(cmin), within distance `maxlen` of L. A sphere that
+    // misses that cone by more than the margins cannot occlude any of them.
+    const bool act = need && !hit;
+    const v3 u = sub(p, L);
+    const float ul = __builtin_sqrtf(dot(u, u));
+    const v3 uh = ul > 0.0f ? muls(u, 1.0f / ul) : mk(0.0f, 0.0f, 0.0f);
+    // cone axis: the direction of the first active lane
+    const int lead = __builtin_ctzll(__ballot(act));
+    const v3 ax = mk(lane_value(uh.x, lead), lane_value(uh.y, lead), lane_value(uh.z, lead));
+    const float cmin = wave_min(act ? dot(ax, uh) : 1.0f);
+    const float maxlen = wave_max(act ? ul : 0.0f);
+    const float al = dot(ax, ax);
+    const bool angular = cmin > 0.0f && al > 0.5f;  // cone narrower than 90 degrees, axis a unit vector
+    const float sth = __builtin_sqrtf(fmaxf(0.0f, 1.0f - cmin * cmin));
+    const int lane = threadIdx.x & 63;
+    for (int base = 0; base < S.ns; base += 64) {
+        const int k = base + lane;
+        bool cand = false;
+        if (k < S.ns) {
+            const float4 c = S.sph[k];
+            const float rad = __int_as_float(S.smeta[k].z);
+            const v3 v = sub(mk(c.x, c.y, c.z), L);
+            const float d = __builtin_sqrtf(dot(v, v));
+            const float rp = rad + 0.021f + 1e-3f * d;  // 0.01 start offset + margins
+            if (d <= rp) {
+                cand = true;
+            } else if (d - rp > maxlen) {
+                cand = false;  // beyond every shaded point
+            } else if (!angular) {
+                cand = true;
+            } else {
+                const float sph = rp / d, cph = __builtin_sqrtf(fmaxf(0.0f, 1.0f - sph * sph));
+                const float cos_lim = cmin * cph - sth * sph;  // cos(theta + phi)
+                cand = !(dot(ax, v) < (cos_lim - 1e-3f) * d);
+            }
+        }
+        uint64_t mask = __ballot(cand);
+        while (mask) {
+            const int s = base + __builtin_ctzll(mask);
+            mask &= mask - 1;
+            exact(s);
+            if (!__any(need && !hit)) return hit;
         }
     }
     return hit;
@@ -256,8 +425,13 @@ struct Collision {
 };
 
 // Build the collision record of the winning object (:628-637, :686-721).
-__device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const Hit &h) {
+__device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const Hit &h, bool valid) {
     Collision c;
+    c.p = mk(0.0f, 0.0f, 0.0f);
+    c.n = mk(0.0f, 0.0f, 1.0f);
+    c.inside = false;
+    c.material = 0;
+    if (!valid) return c;
     if (h.slot >= 0) {
         const float4 sp = S.sph[h.slot];
         const v3 pos = mk(sp.x, sp.y, sp.z);
@@ -269,35 +443,44 @@ __device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const
     } else {
         const BoxRec &B = S.box[~h.slot];
         c.material = B.material;
-        const Slab s = slab(B, xform_point(B.w2l, r.start), xform_dir(B.w2l, r.dir));
-        float isect = s.t_near;
-        v3 boundary = s.t1;
-        c.inside = false;
-        if (s.t_near < 0.0f) {
-            isect = s.t_far;
-            boundary = s.t2;
+        const v3 rs = xform_point(B.w2l, r.start), rd = xform_dir(B.w2l, r.dir);
+        float isect;
+        v3 boundary;
+        if (strictly_inside(B, rs) && not_nan(rd)) {  // t_near < 0: leaving the box
+            boundary = exits(B, rs, rd);
+            isect = gmin(gmin(boundary.x, boundary.y), boundary.z);
             c.inside = true;
+        } else {
+            const Slab s = slab(B, rs, rd);
+            isect = s.t_near;
+            boundary = s.t1;
+            if (s.t_near < 0.0f) {
+                isect = s.t_far;
+                boundary = s.t2;
+                c.inside = true;
+            }
         }
         int face = 0;
         if (isect == boundary.y) face = 1;
         else if (isect == boundary.z) face = 2;
         v3 n = mk(face == 0 ? 1.0f : 0.0f, face == 1 ? 1.0f : 0.0f, face == 2 ? 1.0f : 0.0f);
-        if (comp(s.rd, face) > 0.0f) n = muls(n, -1.0f);
+        if (comp(rd, face) > 0.0f) n = muls(n, -1.0f);
         const float *N = B.nrm;
         c.n = mk(N[0] * n.x + N[1] * n.y + N[2] * n.z, N[3] * n.x + N[4] * n.y + N[5] * n.z,
                  N[6] * n.x + N[7] * n.y + N[8] * n.z);
-        const v3 lp = add(s.rs, muls(s.rd, h.t));
+        const v3 lp = add(rs, muls(rd, h.t));
         c.p = xform_point(B.l2w, lp);
     }
     return c;
 }
 
-// ads_phong_lighting (:789-840).
-__device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collision &c) {
+// ads_phong_lighting (:789-840). Called with all lanes active.
+__device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collision &c, bool valid) {
     const MatRec &m = S.mat[c.material];
     float4 dif = make_float4(0.0f, 0.0f, 0.0f, 0.0f), spe = dif;
     const v3 view = normalize(muls(r.dir, -1.0f));
     for (int j = 0; j < S.nl; ++j) {
+        if (S.light[j].dead != 0.0f) continue;  // no direct term for any material (host-checked)
         const v3 lpos = mk(S.light[j].pos[0], S.light[j].pos[1], S.light[j].pos[2]);
         const v3 ldir = normalize(sub(lpos, c.p));
         const v3 lref = normalize(reflect(muls(ldir, -1.0f), c.n));
@@ -315,9 +498,13 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
             __float_as_uint(nd.z) != __float_as_uint(dif.z) || __float_as_uint(nd.w) != __float_as_uint(dif.w) ||
             __float_as_uint(ns.x) != __float_as_uint(spe.x) || __float_as_uint(ns.y) != __float_as_uint(spe.y) ||
             __float_as_uint(ns.z) != __float_as_uint(spe.z) || __float_as_uint(ns.w) != __float_as_uint(spe.w);
-        if (changes && !occluded(S, add(c.p, muls(c.n, 0.01f)), sub(lpos, c.p))) {
-            dif = nd;
-            spe = ns;
+        const bool need = valid && changes;
+        if (__any(need)) {
+            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sub(lpos, c.p), c.p, lpos, j, need);
+            if (need && !shadowed) {
+                dif = nd;
+                spe = ns;
+            }
         }
     }
     // phong = ambient + diffuse + specular + emissive; return rgb * a (:837-839)
@@ -330,23 +517,27 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
 
 // recursive_raytrace (:1071-1105) as real recursion on a compile-time depth:
 // the stack machine's order (reflection subtree, then refraction subtree,
-// then mix(mix(phong, R, refl), T, transp)) and its flags (:994, :1027).
+// then mix(mix(phong, R, refl), T, transp)), its spawn flags (:994, :1027) and
+// "a missed ray is black" (:962-963). Lanes that do not trace a ray at this
+// level ride along with valid = false.
 template <int kDepth, bool kPrimary>
-__device__ v3 trace(const Scene &S, const Ray &r);
+__device__ v3 trace(const Scene &S, const Ray &r, bool valid);
 
 template <int kDepth, bool kPrimary>
-__device__ __forceinline__ v3 trace_body(const Scene &S, const Ray &r) {
-    const Hit h = closest<kPrimary>(S, r);
-    if (kPrimary && !__any(h.obj >= 0)) return mk(0.0f, 0.0f, 0.0f);  // per-wave early out
-    if (h.obj < 0) return mk(0.0f, 0.0f, 0.0f);                        // miss -> black (:962-963)
-    const Collision c = resolve(S, r, h);
-    v3 col = phong(S, r, c);
+__device__ __forceinline__ v3 trace_body(const Scene &S, const Ray &r, bool valid) {
+    const v3 black = mk(0.0f, 0.0f, 0.0f);
+    const Hit h = closest<kPrimary>(S, r, valid);
+    const bool hit = valid && h.obj >= 0;
+    if (!__any(hit)) return black;  // per-wave early out
+    const Collision c = resolve(S, r, h, hit);
+    v3 col = phong(S, r, c, hit);
     if constexpr (kDepth > 0) {
         const MatRec &m = S.mat[c.material];
 #pragma unroll 1
         for (int k = 0; k < 2; ++k) {
             const float w = k == 0 ? m.reflectivity : m.transparency;
-            if (w > 0.0f) {
+            const bool spawn = hit && w > 0.0f;
+            if (__any(spawn)) {
                 Ray cr;
                 if (k == 0) {
                     cr.start = add(c.p, muls(c.n, 0.001f));
@@ -357,29 +548,60 @@ __device__ __forceinline__ v3 trace_body(const Scene &S, const Ray &r) {
                     if (c.inside) ratio = 1.0f / ratio;
                     cr.dir = refract(r.dir, c.n, ratio);
                 }
-                const v3 cc = trace<kDepth - 1, false>(S, cr);
-                col = mix(col, cc, w);
+                const v3 cc = trace<kDepth - 1, false>(S, cr, spawn);
+                if (spawn) col = mix(col, cc, w);
             }
         }
     }
-    return col;
+    return sel(hit, col, black);
 }
 
 template <int kDepth, bool kPrimary>
-__device__ __noinline__ v3 trace_call(const Scene &S, const Ray &r) {
-    return trace_body<kDepth, kPrimary>(S, r);
+__device__ __noinline__ v3 trace_call(const Scene &S, const Ray &r, bool valid) {
+    return trace_body<kDepth, kPrimary>(S, r, valid);
 }
 
 template <int kDepth, bool kPrimary>
-__device__ __forceinline__ v3 trace(const Scene &S, const Ray &r) {
-    if constexpr (kPrimary || kDepth == 0) return trace_body<kDepth, kPrimary>(S, r);
-    else return trace_call<kDepth, kPrimary>(S, r);
+__device__ __forceinline__ v3 trace(const Scene &S, const Ray &r, bool valid) {
+    if constexpr (kPrimary || kDepth == 0) return trace_body<kDepth, kPrimary>(S, r, valid);
+    else return trace_call<kDepth, kPrimary>(S, r, valid);
 }
 
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     if (p.n_shards <= 0) return p.row_begin + local;
     const int blk = local / p.block_rows;
     return (blk * p.n_shards + p.shard) * p.block_rows + (local - blk * p.block_rows);
+}
+
+// Conservative pixel footprint of a sphere: project the 8 corners of its
+// (inflated) bounding cube with proj*view; valid only when the whole cube is
+// in front of the camera. Two pixels of margin on every side.
+__device__ int4 sphere_footprint(const LaunchParams &p, float4 c, float rad) {
+    const int4 all = make_int4(INT_MIN / 2, INT_MAX / 2, INT_MIN / 2, INT_MAX / 2);
+    const int hw = p.width / 2, hh = p.height / 2;
+    if (!p.cull || hw <= 0 || hh <= 0) return all;
+    const float r = rad * 1.001f + 1e-3f;
+    const float *P = p.proj;
+    float x0 = __builtin_inff(), x1 = -__builtin_inff(), y0 = x0, y1 = x1;
+    bool ok = r == r && c.x == c.x && c.y == c.y && c.z == c.z;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float X = c.x + ((i & 1) ? r : -r), Y = c.y + ((i & 2) ? r : -r), Z = c.z + ((i & 4) ? r : -r);
+        const float cw = P[3] * X + P[7] * Y + P[11] * Z + P[15];
+        const float cx = P[0] * X + P[4] * Y + P[8] * Z + P[12];
+        const float cy = P[1] * X + P[5] * Y + P[9] * Z + P[13];
+        ok = ok && cw > 1e-4f;
+        const float iw = 1.0f / cw;
+        x0 = fminf(x0, cx * iw); x1 = fmaxf(x1, cx * iw);
+        y0 = fminf(y0, cy * iw); y1 = fmaxf(y1, cy * iw);
+    }
+    // pixel x <-> NDC (x - hw) / hw (:377)
+    const float fx0 = floorf(x0 * hw + hw) - 2.0f, fx1 = ceilf(x1 * hw + hw) + 2.0f;
+    const float fy0 = floorf(y0 * hh + hh) - 2.0f, fy1 = ceilf(y1 * hh + hh) + 2.0f;
+    const float lim = 1.0e9f;
+    ok = ok && fabsf(fx0) < lim && fabsf(fx1) < lim && fabsf(fy0) < lim && fabsf(fy1) < lim;
+    if (!ok) return all;
+    return make_int4(static_cast<int>(fx0), static_cast<int>(fx1), static_cast<int>(fy0), static_cast<int>(fy1));
 }
 
 template <int kDepth>
@@ -389,20 +611,23 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     const float4 *blob = static_cast<const float4 *>(p.scene);
     for (int i = threadIdx.x; i < p.blob_units; i += kThreads) lds[i] = blob[i];
     float4 *sph_cam = lds + p.blob_units;
-    float4 *box_cam = sph_cam + p.n_spheres;
+    int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
+    float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
     __syncthreads();
     const v3 origin = mk(p.origin[0], p.origin[1], p.origin[2]);
     {
         const float4 *sph = lds + p.off_spheres;
+        const int4 *smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
         for (int s = threadIdx.x; s < p.n_spheres; s += kThreads) {
             const float4 c = sph[s];
             const v3 oc = sub(origin, mk(c.x, c.y, c.z));
             sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);
+            sph_px[s] = sphere_footprint(p, c, __int_as_float(smeta[s].z));
         }
         const BoxRec *box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
         for (int b = threadIdx.x; b < p.n_boxes; b += kThreads) {
             const v3 rs = xform_point(box[b].w2l, origin);
-            box_cam[b] = make_float4(rs.x, rs.y, rs.z, 0.0f);
+            box_cam[b] = make_float4(rs.x, rs.y, rs.z, strictly_inside(box[b], rs) ? 1.0f : 0.0f);
         }
     }
     __syncthreads();
@@ -410,6 +635,7 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     S.sph = lds + p.off_spheres;
     S.smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
     S.sph_cam = sph_cam;
+    S.sph_px = sph_px;
     S.box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
     S.box_cam = box_cam;
     S.mat = reinterpret_cast<const MatRec *>(lds + p.off_mats);
@@ -418,14 +644,26 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     S.ns = p.n_spheres;
     S.nb = p.n_boxes;
     S.nl = p.n_lights;
+    S.nm = p.n_mats;
+    S.cull = p.cull;
 
     // ---- this lane's pixel: wave w covers the 8x8 quadrant w of the tile ----
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
-    const int local_row = blockIdx.y * kTile + (wave >> 1) * 8 + (lane >> 3);
+    const int lr0 = blockIdx.y * kTile + (wave >> 1) * 8;
+    const int local_row = lr0 + (lane >> 3);
     const bool active = x < p.width && local_row < p.n_rows;
     if (!__any(active)) return;
-    const int y = output_row(p, active ? local_row : 0);
+    const int y = output_row(p, active ? local_row : lr0);
+    S.tx0 = blockIdx.x * kTile + (wave & 1) * 8;
+    S.tx1 = S.tx0 + 7;
+    S.ty0 = INT_MAX;
+    S.ty1 = INT_MIN;
+    for (int i = 0; i < 8; ++i) {
+        const int fy = output_row(p, lr0 + i);
+        S.ty0 = fy < S.ty0 ? fy : S.ty0;
+        S.ty1 = fy > S.ty1 ? fy : S.ty1;
+    }
 
     // ---- camera ray (:377-392) ----
     const int hw = p.width / 2, hh = p.height / 2;
@@ -444,8 +682,7 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     ray.start = origin;
     ray.dir = normalize(sub(e3, s3));
 
-    v3 col = mk(0.0f, 0.0f, 0.0f);
-    if (active) col = trace<kDepth, true>(S, ray);
+    const v3 col = trace<kDepth, true>(S, ray, active);
     if (active) p.out[static_cast<size_t>(local_row) * p.width + x] = make_float4(col.x, col.y, col.z, 0.0f);
 }
 
@@ -459,7 +696,8 @@ hipError_t launch_depth(const LaunchParams &p, hipStream_t stream) {
 }  // namespace
 
 size_t lds_bytes(const LaunchParams &p) {
-    return (static_cast<size_t>(p.blob_units) + p.n_spheres + p.n_boxes) * sizeof(float4);
+    // blob + per-sphere camera terms (16 B) and footprint (16 B) + per-box camera terms
+    return (static_cast<size_t>(p.blob_units) + 2 * static_cast<size_t>(p.n_spheres) + p.n_boxes) * sizeof(float4);
 }
 
 hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t stream) {
@@ -478,10 +716,6 @@ hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t strea
     }
 }
 
-}  // namespace rtamd
-
-namespace rtamd {
-
 // Allow dynamic LDS above the 64 KiB default for every depth instantiation
 // (gfx950 has 160 KiB per CU). Best effort: a failure only lowers the largest
 // scene that fits, which rt_scene_create checks.
@@ -492,7 +726,8 @@ hipError_t allow_large_lds(size_t bytes) {
         reinterpret_cast<const void *>(&render_kernel<4>), reinterpret_cast<const void *>(&render_kernel<5>),
         reinterpret_cast<const void *>(&render_kernel<6>), reinterpret_cast<const void *>(&render_kernel<7>),
         reinterpret_cast<const void *>(&render_kernel<8>), reinterpret_cast<const void *>(&render_kernel<9>)};
-    for (const void *f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+    for (const void *f : fns)
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
     (void)hipGetLastError();  // do not leak a sticky error into the next launch check
     return hipSuccess;
 }

@@ -276,6 +276,48 @@ int rt_make_view(const rt_camera *cam_in, float time, rt_view *out) {
 
 namespace rtamd {
 
+// proj*view for culling: the float64 inverse of the view's unprojection, and
+// whether the view is a consistent pinhole (every pixel's ray, built as the
+// kernel builds it, lies on the line through the origin and its NDC point,
+// with positive homogeneous w) so that projected footprints bound ray hits.
+bool view_projection(const rt_view &v, float proj[16]) {
+    M4 U;
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) U.m[c][r] = v.unprojection[c * 4 + r];
+    const M4 P = inverse(U);
+    bool ok = true;
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) {
+            proj[c * 4 + r] = static_cast<float>(P.m[c][r]);
+            ok = ok && std::isfinite(P.m[c][r]);
+        }
+    const double o[3] = {v.origin[0], v.origin[1], v.origin[2]};
+    const double ndc[5][2] = {{-1, -1}, {1, -1}, {-1, 1}, {1, 1}, {0, 0}};
+    for (int i = 0; i < 5 && ok; ++i) {
+        double pt[2][3];
+        for (int k = 0; k < 2; ++k) {
+            const double z = k == 0 ? 0.5 : 1.0;
+            double h[4];
+            for (int r = 0; r < 4; ++r)
+                h[r] = U.m[0][r] * ndc[i][0] + U.m[1][r] * ndc[i][1] + U.m[2][r] * z + U.m[3][r];
+            ok = ok && h[3] > 0.0;
+            for (int r = 0; r < 3; ++r) pt[k][r] = h[r] / h[3];
+        }
+        // distance of the origin from the line through the two points
+        double d[3], w[3];
+        for (int r = 0; r < 3; ++r) {
+            d[r] = pt[1][r] - pt[0][r];
+            w[r] = o[r] - pt[0][r];
+        }
+        const double dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        const double cx = d[1] * w[2] - d[2] * w[1], cy = d[2] * w[0] - d[0] * w[2], cz = d[0] * w[1] - d[1] * w[0];
+        const double dist = std::sqrt((cx * cx + cy * cy + cz * cz) / dd);
+        const double scale = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) + 1e-12;
+        ok = ok && dd > 0.0 && dist <= 1e-5 * scale;
+    }
+    return ok;
+}
+
 // Build the device blob: [spheres][sphere meta][boxes][materials][lights]
 // [light x material products]; every section 16-B aligned.
 int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
@@ -311,6 +353,21 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             std::memcpy(b.maxs, o.box_maxs, 12);
             b.obj_index = i;
             b.material = o.material;
+            // Lights strictly inside the box by a margin (float64): a shadow
+            // segment that starts inside the box then ends inside it too (its
+            // end is the light + 0.01 n, :808-809), so the box cannot occlude.
+            for (int j = 0; j < n_lights && j < 32; ++j) {
+                double lp[3];
+                bool in = true;
+                for (int r = 0; r < 3; ++r) {
+                    lp[r] = W.m[0][r] * lights[j].position[0] + W.m[1][r] * lights[j].position[1] +
+                            W.m[2][r] * lights[j].position[2] + W.m[3][r];
+                    const double m = 0.05 + 1e-4 * (std::fabs(o.box_mins[r]) + std::fabs(o.box_maxs[r]) +
+                                                    std::fabs(lp[r]));
+                    in = in && std::isfinite(lp[r]) && o.box_mins[r] + m < lp[r] && lp[r] < o.box_maxs[r] - m;
+                }
+                if (in) b.light_inside |= 1u << j;
+            }
             boxes.push_back(b);
         }
     }
@@ -334,10 +391,22 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
                 lm[m * n_lights + j].ls_ms[k] = lights[j].specular[k] * mats[m].specular[k];  // :832
             }
     }
+    // A light with zero diffuse and specular colour (the reference's ambient
+    // light, :202-207) adds +-0 to the sums for every finite material with
+    // shininess >= 0 (pow then stays finite), so lit and shadowed agree and
+    // the kernel may skip it; its ambient term is in amb_sum.
+    bool materials_tame = true;
+    for (int m = 0; m < n_mats; ++m) {
+        materials_tame = materials_tame && mats[m].shininess >= 0.0f;
+        for (int k = 0; k < 4; ++k)
+            materials_tame = materials_tame && std::isfinite(mats[m].diffuse[k]) && std::isfinite(mats[m].specular[k]);
+    }
     std::vector<LightRec> lrec(n_lights);
     for (int j = 0; j < n_lights; ++j) {
         std::memcpy(lrec[j].pos, lights[j].position, 12);
-        lrec[j].pad = 0.0f;
+        bool zero = true;
+        for (int k = 0; k < 4; ++k) zero = zero && lights[j].diffuse[k] == 0.0f && lights[j].specular[k] == 0.0f;
+        lrec[j].dead = (zero && materials_tame) ? 1.0f : 0.0f;
     }
     auto units = [](size_t bytes) { return static_cast<int32_t>((bytes + 15) / 16); };
     int32_t off = 0;
