@@ -187,6 +187,14 @@ int rt_last_kernel_ms(rt_context *ctx, float *ms);
  * it (clamp to [0,1], round to nearest). Host memory, n pixels. */
 int rt_pack_rgba8(const float *rgba32f, size_t n_pixels, uint8_t *out_rgba8);
 
+/* Headless image dump (replaces the display pass, draw_screen_*.glsl and
+ * main.cpp:240-260). `rgba32f` is a frame in this ABI's layout (row 0 = GL's
+ * bottom row). PPM: binary P6, 8-bit, RGBA8 unorm rounding (rt_pack_rgba8),
+ * rows written top-down (the on-screen orientation). PFM: float RGB, rows
+ * bottom-up as the PFM format stores them, little-endian. */
+int rt_write_ppm(const char *path, const float *rgba32f, int width, int height);
+int rt_write_pfm(const char *path, const float *rgba32f, int width, int height);
+
 const char *rt_last_error(void);
 const char *rt_version(void);
 

@@ -66,6 +66,7 @@ def lib():
             "rt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i),
             "rt_context_set": ([vp, i, i], i),
             "rt_pack_rgba8": ([vp, C.c_size_t, vp], i),
+            "rt_write_ppm": ([C.c_char_p, vp, i, i], i), "rt_write_pfm": ([C.c_char_p, vp, i, i], i),
             "rt_last_error": ([], C.c_char_p), "rt_version": ([], C.c_char_p),
         }
         for name, (args, res) in sig.items():
@@ -145,6 +146,18 @@ def pack_rgba8(rgba):
     out = np.zeros(a.shape, np.uint8)
     _check(lib().rt_pack_rgba8(a.ctypes.data, a.size // 4, out.ctypes.data))
     return out
+
+
+def write_ppm(path, rgba):
+    """8-bit PPM of a frame (RGBA8 rounding, top row first)."""
+    a = np.ascontiguousarray(rgba, np.float32)
+    _check(lib().rt_write_ppm(os.fsencode(path), a.ctypes.data, a.shape[1], a.shape[0]))
+
+
+def write_pfm(path, rgba):
+    """Float PFM of a frame (bottom row first, little-endian)."""
+    a = np.ascontiguousarray(rgba, np.float32)
+    _check(lib().rt_write_pfm(os.fsencode(path), a.ctypes.data, a.shape[1], a.shape[0]))
 
 
 class Context:

@@ -1,0 +1,104 @@
+// rt_cli — headless frame driver: the counterpart of the reference's
+// main()/draw() loop (OpenGLRaytracer/main.cpp:47-93, :210-261) without a
+// window. Renders the shipped scene (or a benchmark scene) at `time`, K frames
+// apart by `dt` (the orbiting camera and animated boxes, :334-364, :261-321),
+// and writes each frame as PPM (what the RGBA8 surface shows) and/or PFM.
+//
+//   rt_cli [--width 1280] [--height 720] [--depth 0] [--time 0] [--frames 1]
+//          [--dt 0.016] [--scene shipped|spheres:N[:seed]] [--ppm out_%04d.ppm]
+//          [--pfm out_%04d.pfm] [--device 0]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+
+namespace {
+
+int fail(const char *what) {
+    std::fprintf(stderr, "rt_cli: %s: %s\n", what, rt_last_error());
+    return 1;
+}
+
+std::string frame_name(const std::string &pattern, int k) {
+    if (pattern.find('%') == std::string::npos) return pattern;
+    char buf[4096];
+    std::snprintf(buf, sizeof buf, pattern.c_str(), k);
+    return buf;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    int width = 1280, height = 720, depth = 0, frames = 1, device = 0;  // main.cpp:17-19
+    float time0 = 0.0f, dt = 1.0f / 60.0f;
+    std::string scene = "shipped", ppm, pfm;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> const char * {
+            if (i + 1 >= argc) { std::fprintf(stderr, "rt_cli: %s needs a value\n", a.c_str()); std::exit(2); }
+            return argv[++i];
+        };
+        if (a == "--width") width = std::atoi(next());
+        else if (a == "--height") height = std::atoi(next());
+        else if (a == "--depth") depth = std::atoi(next());
+        else if (a == "--time") time0 = std::strtof(next(), nullptr);
+        else if (a == "--frames") frames = std::atoi(next());
+        else if (a == "--dt") dt = std::strtof(next(), nullptr);
+        else if (a == "--scene") scene = next();
+        else if (a == "--ppm") ppm = next();
+        else if (a == "--pfm") pfm = next();
+        else if (a == "--device") device = std::atoi(next());
+        else {
+            std::fprintf(stderr, "usage: rt_cli [--width W] [--height H] [--depth D] [--time T] [--frames K] "
+                                 "[--dt S] [--scene shipped|spheres:N[:seed]] [--ppm PAT] [--pfm PAT] [--device I]\n");
+            return 2;
+        }
+    }
+    rt_context *ctx = nullptr;
+    if (rt_create(device, &ctx) != RT_OK) return fail("rt_create");
+    rt_material mats[RT_REFERENCE_MATERIALS];
+    rt_light lights[RT_REFERENCE_LIGHTS];
+    rt_reference_materials(mats);
+    rt_reference_lights(lights);
+    std::vector<float> frame(static_cast<size_t>(width) * height * 4);
+    for (int k = 0; k < frames; ++k) {
+        const float t = time0 + k * dt;
+        std::vector<rt_object> objs;
+        if (scene == "shipped") {
+            objs.resize(RT_REFERENCE_OBJECTS);
+            rt_reference_objects(t, objs.data());
+        } else if (scene.rfind("spheres:", 0) == 0) {
+            int n = 0;
+            unsigned long long seed = 0;
+            std::sscanf(scene.c_str() + 8, "%d:%llu", &n, &seed);
+            objs.resize(static_cast<size_t>(n) + 1);
+            if (rt_bench_objects(n, seed, objs.data()) != RT_OK) return fail("rt_bench_objects");
+        } else {
+            std::fprintf(stderr, "rt_cli: unknown scene %s\n", scene.c_str());
+            return 2;
+        }
+        rt_scene *sc = nullptr;
+        if (rt_scene_create(ctx, objs.data(), static_cast<int>(objs.size()), mats, RT_REFERENCE_MATERIALS, lights,
+                            RT_REFERENCE_LIGHTS, &sc) != RT_OK)
+            return fail("rt_scene_create");
+        const auto t0 = std::chrono::steady_clock::now();
+        if (rt_render(ctx, sc, nullptr, t, width, height, depth, 0, height, frame.data(), 0, nullptr) != RT_OK)
+            return fail("rt_render");
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        float kms = 0.0f;
+        rt_last_kernel_ms(ctx, &kms);
+        std::printf("frame %d t=%.4f  kernel %.3f ms  call %.3f ms (incl. device->host copy)\n", k, t, kms,
+                    wall * 1e3);
+        if (!ppm.empty() && rt_write_ppm(frame_name(ppm, k).c_str(), frame.data(), width, height) != RT_OK)
+            return fail("rt_write_ppm");
+        if (!pfm.empty() && rt_write_pfm(frame_name(pfm, k).c_str(), frame.data(), width, height) != RT_OK)
+            return fail("rt_write_pfm");
+        rt_scene_destroy(sc);
+    }
+    rt_destroy(ctx);
+    return 0;
+}

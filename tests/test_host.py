@@ -133,3 +133,25 @@ def test_product_does_not_import_the_oracle():
                     text = f.read()
                 assert "oracle" not in re.sub(r"(#|//).*", "", text).lower().replace(
                     "oracle/rt_oracle.c", ""), fn
+
+
+def test_ppm_and_pfm_dump(tmp_path):
+    rng = np.random.default_rng(1)
+    h, w = 5, 7
+    img = (rng.random((h, w, 4)) * 1.4 - 0.2).astype(np.float32)
+    img[..., 3] = 0
+    ppm, pfm = str(tmp_path / "a.ppm"), str(tmp_path / "a.pfm")
+    rt.write_ppm(ppm, img)
+    rt.write_pfm(pfm, img)
+    raw = open(ppm, "rb").read()
+    head = b"P6\n%d %d\n255\n" % (w, h)
+    assert raw.startswith(head)
+    pix = np.frombuffer(raw[len(head):], np.uint8).reshape(h, w, 3)
+    assert np.array_equal(pix, rt.pack_rgba8(img)[::-1, :, :3])  # GL row 0 = bottom row
+    raw = open(pfm, "rb").read()
+    head = b"PF\n%d %d\n-1.0\n" % (w, h)
+    assert raw.startswith(head)
+    f = np.frombuffer(raw[len(head):], "<f4").reshape(h, w, 3)
+    assert np.array_equal(f, img[..., :3])  # PFM rows are bottom-up, like GL
+    with pytest.raises(rt.RTError):
+        rt.write_ppm(str(tmp_path / "missing" / "x.ppm"), img)
