@@ -6,10 +6,11 @@ max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
 
 A step renders N frames of 1920x1080 (N = number of GPUs; frame k is the
 reference orbit camera at time k/60 s). Every frame is row-tiled across the N
-ranks in interleaved 8-row blocks (rt_render_shard); rank 0 assembles the N
-frames with one RCCL gather over xGMI plus a row de-interleave. Per-GPU work
-is one frame per step at every N: weak scaling. At N=1 a step is one full
-frame rendered in place (no collective).
+ranks in interleaved 8-row blocks; each rank renders its blocks of all N
+frames in one launch (rt_render_batch), and rank 0 assembles the N frames with
+one RCCL gather over xGMI plus a row de-interleave. Per-GPU work is one frame
+per step at every N: weak scaling. At N=1 a step is one full frame rendered
+in place (no collective).
 
 value = primary rays of all frames / step time (max over ranks), Mrays/s.
 roofline = the render kernel against the HBM-write roofline: 16 B per pixel
@@ -106,36 +107,30 @@ def main():
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
 
-    if world == 1:
-        frames = torch.empty((1, HEIGHT, WIDTH, 4), dtype=torch.float32, device="cuda")
-        shard_rows = HEIGHT
-    else:
-        shard_rows = max(rt.shard_rows(HEIGHT, BLOCK_ROWS, world, s) for s in range(world))
-        shard = torch.zeros((n_frames, shard_rows, WIDTH, 4), dtype=torch.float32, device="cuda")
-        gathered = [torch.empty_like(shard) for _ in range(world)] if rank == 0 else None
-        frames = None
+    # every launch renders this rank's rows of all n_frames frames
+    # (rt_render_batch: blockIdx.z = frame); N=1 renders whole frames in place
+    rows_mine = HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
+    flat_elems = frame.flat_shard_elems(n_frames, HEIGHT, WIDTH, BLOCK_ROWS, world)
+    buf = torch.zeros(flat_elems, dtype=torch.float32, device="cuda")
+    gathered = [torch.empty_like(buf) for _ in range(world)] if (world > 1 and rank == 0) else None
+    perm = torch.as_tensor(frame.assembly_permutation(HEIGHT, BLOCK_ROWS, world), device="cuda")
 
     # HIP events around every render launch of the timed region, on the
     # stream the kernel is launched on
-    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(n_frames)] for _ in range(args.steps)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
 
     def step(timed, it=0):
-        for k in range(n_frames):
-            if timed:
-                ev[it][k][0].record(stream)
-            if world == 1:
-                rt.render_device(ctx, scene, frames[k].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH,
-                                 view=views[k], stream=sh)
-            else:
-                rt.render_shard(ctx, scene, shard[k].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, BLOCK_ROWS,
-                                world, rank, view=views[k], stream=sh)
-            if timed:
-                ev[it][k][1].record(stream)
+        if timed:
+            ev[it][0].record(stream)
+        rt.render_batch(ctx, scene, buf.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS,
+                        world, rank, stream=sh)
+        if timed:
+            ev[it][1].record(stream)
         if world > 1:
-            dist.gather(shard, gathered, dst=0)
-            if rank == 0:
-                frame.assemble(gathered, HEIGHT, BLOCK_ROWS)  # (n_frames, H, W, 4), row order restored
+            dist.gather(buf, gathered, dst=0)
+            if rank == 0:  # (n_frames, H, W, 4) in frame row order
+                frame.assemble(gathered, n_frames, HEIGHT, WIDTH, BLOCK_ROWS, perm=perm)
 
     for _ in range(args.warmup):
         step(False)
@@ -151,7 +146,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kernel_ms = [a.elapsed_time(b) for row in ev for a, b in row]
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -160,7 +155,7 @@ def main():
     rays = n_frames * WIDTH * HEIGHT * args.steps
     value = rays / elapsed / 1e6
     avg_kernel_ms = float(np.mean(kernel_ms))
-    px_per_launch = WIDTH * (HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank))
+    px_per_launch = WIDTH * rows_mine * n_frames
     achieved = px_per_launch * BYTES_PER_PIXEL / (avg_kernel_ms * 1e-3) / 1e9
     traffic = pmc_traffic() if world == 1 else None
     if rank == 0:

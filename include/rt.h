@@ -173,6 +173,15 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
                     int height, int max_depth, int block_rows, int n_shards, int shard,
                     float *out_device, void *hip_stream);
 
+/* Several frames in one launch (the reference's frame loop, main.cpp:81-86,
+ * batched): views[k] renders into out_device + k * rows * width * 4 floats,
+ * where rows = height, or rt_shard_rows(...) when n_shards > 1 (each frame
+ * then gets this shard's interleaved row blocks). The scene is shared. */
+#define RT_MAX_BATCH 8
+int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views, int width,
+                    int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
+                    void *hip_stream);
+
 /* Context options. RT_OPT_CULLING (default 1): skip spheres that provably
  * cannot be hit (conservative footprints / light cones with margins far
  * above float error) — output is bit-identical either way. */

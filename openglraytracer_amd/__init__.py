@@ -65,6 +65,7 @@ def lib():
             "rt_render_shard": ([vp, vp, vp, i, i, i, i, i, i, vp, vp], i),
             "rt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i),
             "rt_context_set": ([vp, i, i], i),
+            "rt_render_batch": ([vp, vp, vp, i, i, i, i, i, i, i, vp, vp], i),
             "rt_pack_rgba8": ([vp, C.c_size_t, vp], i),
             "rt_write_ppm": ([C.c_char_p, vp, i, i], i), "rt_write_pfm": ([C.c_char_p, vp, i, i], i),
             "rt_last_error": ([], C.c_char_p), "rt_version": ([], C.c_char_p),
@@ -246,6 +247,16 @@ def render_device(ctx, scene, out_ptr, width, height, max_depth=0, view=None, ro
     _check(lib().rt_render_view(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
                                 r0, r1, C.c_void_p(out_ptr), 1,
                                 C.c_void_p(stream) if stream else None))
+
+
+def render_batch(ctx, scene, out_ptr, width, height, max_depth, views, block_rows=8, n_shards=1,
+                 shard=0, stream=None):
+    """K frames (K = len(views) <= 8) in one launch into device memory laid
+    out (K, rows, width, 4); rows = height, or this shard's rows."""
+    arr = (View * len(views))(*views)
+    _check(lib().rt_render_batch(ctx.handle, scene.handle, arr, len(views), width, height, max_depth,
+                                 block_rows, n_shards, shard, C.c_void_p(out_ptr),
+                                 C.c_void_p(stream) if stream else None))
 
 
 def render_shard(ctx, scene, out_ptr, width, height, max_depth, block_rows, n_shards, shard,

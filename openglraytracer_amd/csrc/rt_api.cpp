@@ -61,12 +61,16 @@ int check_render_args(const rt_context *ctx, const rt_scene *scene, int width, i
     return RT_OK;
 }
 
-LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_view *view, int width,
-                         int height) {
+LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views,
+                         int width, int height) {
     LaunchParams p{};
-    p.cull = (view_projection(*view, p.proj) && ctx->culling) ? 1 : 0;
-    std::memcpy(p.unproj, view->unprojection, sizeof p.unproj);
-    std::memcpy(p.origin, view->origin, sizeof p.origin);
+    p.n_views = n_views;
+    for (int k = 0; k < n_views; ++k) {
+        FrameView &v = p.view[k];
+        v.cull = (view_projection(views[k], v.proj) && ctx->culling) ? 1 : 0;
+        std::memcpy(v.unproj, views[k].unprojection, sizeof v.unproj);
+        std::memcpy(v.origin, views[k].origin, sizeof v.origin);
+    }
     p.width = width;
     p.height = height;
     const DeviceScene &d = scene->dev;
@@ -81,6 +85,8 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.off_mats = d.off_mats;
     p.off_lights = d.off_lights;
     p.off_lightmat = d.off_lightmat;
+    p.off_bvh = d.off_bvh;
+    p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
     return p;
 }
@@ -207,7 +213,7 @@ int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, 
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail("hipSetDevice", e);
-    LaunchParams p = base_params(ctx, scene, view, width, height);
+    LaunchParams p = base_params(ctx, scene, view, 1, width, height);
     p.row_begin = row_begin;
     p.n_rows = row_end - row_begin;
     const size_t n_px = static_cast<size_t>(p.n_rows) * width;
@@ -269,12 +275,49 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
     if (rows == 0) return RT_OK;
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail("hipSetDevice", e);
-    LaunchParams p = base_params(ctx, scene, view, width, height);
+    LaunchParams p = base_params(ctx, scene, view, 1, width, height);
     p.row_begin = 0;
     p.n_rows = rows;
     p.block_rows = block_rows;
     p.n_shards = n_shards;
     p.shard = shard;
+    p.out = reinterpret_cast<float4 *>(out_device);
+    hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    rc = launch(ctx, p, max_depth, stream);
+    if (rc != RT_OK) return rc;
+    if (!hip_stream) {
+        e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail("render", e);
+    }
+    return RT_OK;
+}
+
+int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views, int width,
+                    int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
+                    void *hip_stream) {
+    int rc = check_render_args(ctx, scene, width, height, max_depth);
+    if (rc != RT_OK) return rc;
+    if (!views || n_views <= 0 || n_views > RT_MAX_BATCH || !out_device) {
+        set_error("rt_render_batch: need 1.." + std::to_string(RT_MAX_BATCH) + " views and a device output");
+        return RT_ERR_INVALID;
+    }
+    const bool sharded = n_shards > 1;
+    const int rows = sharded ? rt_shard_rows(height, block_rows, n_shards, shard) : height;
+    if (rows < 0 || (n_shards > 1 && block_rows <= 0)) {
+        set_error("rt_render_batch: bad shard arguments");
+        return RT_ERR_INVALID;
+    }
+    if (rows == 0) return RT_OK;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    LaunchParams p = base_params(ctx, scene, views, n_views, width, height);
+    p.row_begin = 0;
+    p.n_rows = rows;
+    if (sharded) {
+        p.block_rows = block_rows;
+        p.n_shards = n_shards;
+        p.shard = shard;
+    }
     p.out = reinterpret_cast<float4 *>(out_device);
     hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
     rc = launch(ctx, p, max_depth, stream);

@@ -24,7 +24,7 @@ struct SphereRec {
 struct SphereMeta {
     int32_t obj_index;
     int32_t material;
-    float radius;  // kept for completeness (intersection uses rr)
+    float radius;  // |radius|, for the culling bounds (intersection uses rr)
     int32_t pad;
 };
 
@@ -57,31 +57,54 @@ struct LightMatRec {
     float ld_md[4];
     float ls_ms[4];
 };  // 32 B
+// Sphere BVH node (depth-first order; the left child is the next node):
+// lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
+// this subtree (-1: end) and leaf = (count << 24) | first sphere slot (0 for
+// an inner node). Bounds are the spheres' boxes inflated by a margin far
+// above float error, so the approximate box test never drops a sphere the
+// exact test could hit.
+struct BvhNode {
+    float lo[3];
+    int32_t skip;
+    float hi[3];
+    int32_t leaf;
+};
+static_assert(sizeof(BvhNode) == 32, "BvhNode layout");
+
 struct LightRec {
     float pos[3];
     float dead;  // 1: zero diffuse and specular for every material (no direct term, no shadow ray)
 };
 
 // Per-launch parameters (kernarg, read through the scalar cache).
-struct LaunchParams {
+// Per-frame camera constants of one view of a launch.
+struct FrameView {
     float unproj[16];  // column-major inverse(proj*view) (:383)
+    float proj[16];    // column-major proj*view = inverse(unproj) (float64 on the host), for culling
     float origin[3];   // ray start = camera position (:391)
+    int32_t cull;      // 1: exactness-preserving culling enabled (consistent pinhole view)
+};
+constexpr int kMaxViews = 8;  // frames per launch (blockIdx.z)
+
+struct LaunchParams {
+    FrameView view[kMaxViews];
+    int32_t n_views;
     int32_t width, height;
     int32_t row_begin, n_rows;          // contiguous band [row_begin, row_begin+n_rows)
     int32_t block_rows, n_shards, shard;  // interleaved shard mapping when n_shards > 0
     int32_t n_spheres, n_boxes, n_mats, n_lights;
     const void *scene;  // device blob
-    float4 *out;        // n_rows * width float4
+    float4 *out;        // n_views x n_rows x width float4
     int32_t off_spheres, off_smeta, off_boxes, off_mats, off_lights, off_lightmat;  // 16-B units
-    int32_t blob_units;                                                         // blob size, 16-B units
-    float proj[16];  // column-major proj*view = inverse(unproj) (float64 on the host), for culling
-    int32_t cull;    // 1: exactness-preserving culling enabled (consistent pinhole view)
+    int32_t off_bvh, n_bvh;  // sphere BVH nodes (2 x float4 each), 16-B units / count
+    int32_t blob_units;      // blob size, 16-B units
 };
 
 struct DeviceScene {
     void *blob = nullptr;
     int32_t blob_units = 0;
     int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
+    int32_t off_bvh = 0, n_bvh = 0;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
 

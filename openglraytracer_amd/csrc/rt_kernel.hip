@@ -149,7 +149,8 @@ struct Scene {
     const MatRec *mat;
     const LightRec *light;
     const LightMatRec *lm;
-    int ns, nb, nl, nm;
+    const float4 *bvh;  // BvhNode pairs (lo, hi)
+    int ns, nb, nl, nm, nbvh;
     int cull;
     int tx0, tx1, ty0, ty1;  // this wave's pixel rectangle (frame coordinates)
 };
@@ -290,6 +291,30 @@ __device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 
     }
 }
 
+// Conservative ray / inflated-box overlap for the BVH: approximate reciprocal
+// direction, slack relative to |t|. The node boxes are inflated on the host
+// by far more than the error of this test, so it never rejects a box whose
+// spheres the exact test could hit; t_max of the node is compared with the
+// running closest t (a sphere's t is at least its box's entry distance).
+struct RayInv {
+    v3 o, id;
+};
+__device__ __forceinline__ float safe_rcp(float d) {
+    return fabsf(d) > 1e-30f ? __builtin_amdgcn_rcpf(d) : (__float_as_uint(d) >> 31 ? -1e30f : 1e30f);
+}
+__device__ __forceinline__ RayInv ray_inv(const Ray &r) {
+    return {r.start, mk(safe_rcp(r.dir.x), safe_rcp(r.dir.y), safe_rcp(r.dir.z))};
+}
+__device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, float t_limit) {
+    const float x0 = (lo.x - q.o.x) * q.id.x, x1 = (hi.x - q.o.x) * q.id.x;
+    const float y0 = (lo.y - q.o.y) * q.id.y, y1 = (hi.y - q.o.y) * q.id.y;
+    const float z0 = (lo.z - q.o.z) * q.id.z, z1 = (hi.z - q.o.z) * q.id.z;
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    const float slack = 1e-5f * (fabsf(tn) + fabsf(tf)) + 1e-6f;
+    return tn <= tf + slack && tf >= -slack && tn <= t_limit + 1e-5f * fabsf(t_limit) + slack;
+}
+
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
 __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
@@ -327,6 +352,25 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
                 const int s = base + __builtin_ctzll(mask);
                 mask &= mask - 1;
                 test_sphere(S, s, r.start, d2, qa2, qa4, true, h);
+            }
+        }
+    } else if (!kPrimary && S.cull && S.nbvh > 0) {
+        // secondary rays: stackless depth-first BVH walk (skip links)
+        const RayInv q = ray_inv(r);
+        int node = valid ? 0 : -1;
+        while (node >= 0) {
+            const float4 lo = S.bvh[2 * node], hi = S.bvh[2 * node + 1];
+            const int leaf = __float_as_int(hi.w);
+            if (node_hit(q, lo, hi, h.t)) {
+                if (leaf) {
+                    const int first = leaf & 0xFFFFFF, count = leaf >> 24;
+                    for (int s = first; s < first + count; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, false, h);
+                    node = __float_as_int(lo.w);
+                } else {
+                    node = node + 1;
+                }
+            } else {
+                node = __float_as_int(lo.w);
             }
         }
     } else {
@@ -576,12 +620,12 @@ __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
 // Conservative pixel footprint of a sphere: project the 8 corners of its
 // (inflated) bounding cube with proj*view; valid only when the whole cube is
 // in front of the camera. Two pixels of margin on every side.
-__device__ int4 sphere_footprint(const LaunchParams &p, float4 c, float rad) {
+__device__ int4 sphere_footprint(const LaunchParams &p, const FrameView &V, float4 c, float rad) {
     const int4 all = make_int4(INT_MIN / 2, INT_MAX / 2, INT_MIN / 2, INT_MAX / 2);
     const int hw = p.width / 2, hh = p.height / 2;
-    if (!p.cull || hw <= 0 || hh <= 0) return all;
+    if (!V.cull || hw <= 0 || hh <= 0) return all;
     const float r = rad * 1.001f + 1e-3f;
-    const float *P = p.proj;
+    const float *P = V.proj;
     float x0 = __builtin_inff(), x1 = -__builtin_inff(), y0 = x0, y1 = x1;
     bool ok = r == r && c.x == c.x && c.y == c.y && c.z == c.z;
 #pragma unroll
@@ -614,7 +658,8 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
     float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
     __syncthreads();
-    const v3 origin = mk(p.origin[0], p.origin[1], p.origin[2]);
+    const FrameView &V = p.view[blockIdx.z];
+    const v3 origin = mk(V.origin[0], V.origin[1], V.origin[2]);
     {
         const float4 *sph = lds + p.off_spheres;
         const int4 *smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
@@ -622,7 +667,7 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
             const float4 c = sph[s];
             const v3 oc = sub(origin, mk(c.x, c.y, c.z));
             sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);
-            sph_px[s] = sphere_footprint(p, c, __int_as_float(smeta[s].z));
+            sph_px[s] = sphere_footprint(p, V, c, __int_as_float(smeta[s].z));
         }
         const BoxRec *box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
         for (int b = threadIdx.x; b < p.n_boxes; b += kThreads) {
@@ -641,11 +686,13 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     S.mat = reinterpret_cast<const MatRec *>(lds + p.off_mats);
     S.light = reinterpret_cast<const LightRec *>(lds + p.off_lights);
     S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
+    S.bvh = lds + p.off_bvh;
+    S.nbvh = p.n_bvh;
     S.ns = p.n_spheres;
     S.nb = p.n_boxes;
     S.nl = p.n_lights;
     S.nm = p.n_mats;
-    S.cull = p.cull;
+    S.cull = V.cull;
 
     // ---- this lane's pixel: wave w covers the 8x8 quadrant w of the tile ----
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -669,7 +716,7 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     const int hw = p.width / 2, hh = p.height / 2;
     const float vx = static_cast<float>(x - hw) / static_cast<float>(hw);
     const float vy = static_cast<float>(y - hh) / static_cast<float>(hh);
-    const float *M = p.unproj;  // column-major
+    const float *M = V.unproj;  // column-major
     float ws[4], we[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -683,12 +730,13 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     ray.dir = normalize(sub(e3, s3));
 
     const v3 col = trace<kDepth, true>(S, ray, active);
-    if (active) p.out[static_cast<size_t>(local_row) * p.width + x] = make_float4(col.x, col.y, col.z, 0.0f);
+    float4 *out = p.out + static_cast<size_t>(blockIdx.z) * p.n_rows * p.width;
+    if (active) out[static_cast<size_t>(local_row) * p.width + x] = make_float4(col.x, col.y, col.z, 0.0f);
 }
 
 template <int kDepth>
 hipError_t launch_depth(const LaunchParams &p, hipStream_t stream) {
-    const dim3 grid((p.width + kTile - 1) / kTile, (p.n_rows + kTile - 1) / kTile);
+    const dim3 grid((p.width + kTile - 1) / kTile, (p.n_rows + kTile - 1) / kTile, p.n_views);
     hipLaunchKernelGGL(render_kernel<kDepth>, grid, dim3(kThreads), lds_bytes(p), stream, p);
     return hipGetLastError();
 }

@@ -9,6 +9,7 @@
 // re-associates inexact float ops, so no float order reproduces it — float64
 // is the closest independent estimate ("Parity").
 // Everything the kernel evaluates per pixel stays float32 in GLSL order.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -276,6 +277,105 @@ int rt_make_view(const rt_camera *cam_in, float time, rt_view *out) {
 
 namespace rtamd {
 
+namespace {
+
+// Build a BVH over the spheres with finite centre and radius (the others can
+// never produce a valid hit: their quadratic is NaN or its roots infinite),
+// reordering `sph`/`smeta` into leaf order. Median split on the widest
+// centroid axis, leaves of <= 4 spheres, depth-first layout with skip links.
+struct BuildItem {
+    SphereRec s;
+    SphereMeta m;
+    double lo[3], hi[3], c[3];
+};
+
+int build_node(std::vector<BuildItem> &items, int begin, int end, std::vector<BvhNode> &nodes) {
+    const int id = static_cast<int>(nodes.size());
+    nodes.push_back(BvhNode{});
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    double clo[3] = {1e300, 1e300, 1e300}, chi[3] = {-1e300, -1e300, -1e300};
+    for (int i = begin; i < end; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], items[i].lo[a]);
+            hi[a] = std::max(hi[a], items[i].hi[a]);
+            clo[a] = std::min(clo[a], items[i].c[a]);
+            chi[a] = std::max(chi[a], items[i].c[a]);
+        }
+    BvhNode &n = nodes[id];
+    for (int a = 0; a < 3; ++a) {
+        n.lo[a] = std::nextafter(static_cast<float>(lo[a]), -INFINITY);
+        n.hi[a] = std::nextafter(static_cast<float>(hi[a]), INFINITY);
+    }
+    if (end - begin <= 4) {
+        n.leaf = ((end - begin) << 24) | begin;
+        return id;
+    }
+    int axis = 0;
+    for (int a = 1; a < 3; ++a)
+        if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+    const int mid = (begin + end) / 2;
+    std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
+                     [axis](const BuildItem &x, const BuildItem &y) { return x.c[axis] < y.c[axis]; });
+    nodes[id].leaf = 0;
+    build_node(items, begin, mid, nodes);
+    build_node(items, mid, end, nodes);
+    return id;
+}
+
+// Subtree sizes make the skip links: in depth-first order a subtree rooted at
+// id occupies [id, id + size).
+int subtree_size(const std::vector<BvhNode> &nodes, int id) {
+    if (nodes[id].leaf) return 1;
+    const int left = subtree_size(nodes, id + 1);
+    return 1 + left + subtree_size(nodes, id + 1 + left);
+}
+
+void set_skips(std::vector<BvhNode> &nodes, int id, int next) {
+    nodes[id].skip = next;
+    if (nodes[id].leaf) return;
+    const int left = id + 1, left_size = subtree_size(nodes, left);
+    const int right = left + left_size;
+    set_skips(nodes, left, right);
+    set_skips(nodes, right, next);
+}
+
+void build_bvh(std::vector<SphereRec> &sph, std::vector<SphereMeta> &smeta, std::vector<BvhNode> &nodes) {
+    std::vector<BuildItem> finite, other;
+    for (size_t i = 0; i < sph.size(); ++i) {
+        BuildItem it{sph[i], smeta[i], {}, {}, {}};
+        const double c[3] = {sph[i].cx, sph[i].cy, sph[i].cz};
+        const double r = std::sqrt(static_cast<double>(sph[i].rr));  // |radius| as the test sees it
+        bool ok = std::isfinite(r);
+        double mag = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            ok = ok && std::isfinite(c[a]);
+            mag = std::max(mag, std::fabs(c[a]) + r);
+        }
+        const double margin = 1e-3 + 1e-4 * mag;
+        for (int a = 0; a < 3; ++a) {
+            it.c[a] = c[a];
+            it.lo[a] = c[a] - r - margin;
+            it.hi[a] = c[a] + r + margin;
+        }
+        (ok ? finite : other).push_back(it);
+    }
+    nodes.clear();
+    if (!finite.empty()) {
+        build_node(finite, 0, static_cast<int>(finite.size()), nodes);
+        set_skips(nodes, 0, -1);
+    }
+    // leaf order first, then the spheres that cannot be hit (linear loops only)
+    sph.clear();
+    smeta.clear();
+    for (auto *v : {&finite, &other})
+        for (const BuildItem &it : *v) {
+            sph.push_back(it.s);
+            smeta.push_back(it.m);
+        }
+}
+
+}  // namespace
+
 // proj*view for culling: the float64 inverse of the view's unprojection, and
 // whether the view is a consistent pinhole (every pixel's ray, built as the
 // kernel builds it, lies on the line through the origin and its NDC point,
@@ -335,7 +435,9 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         }
         if (kind == 2) {
             sph.push_back({o.position[0], o.position[1], o.position[2], o.radius * o.radius});
-            smeta.push_back({i, o.material, o.radius, 0});
+            // |radius| for the culling bounds (a negative radius other than -1
+            // is a sphere of radius |r|: the test only sees r*r, :588)
+            smeta.push_back({i, o.material, std::fabs(o.radius), 0});
         } else {
             const M4 L = transform(o.position, o.angles);
             const M4 W = inverse(L);
@@ -371,6 +473,8 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             boxes.push_back(b);
         }
     }
+    std::vector<BvhNode> bvh;
+    build_bvh(sph, smeta, bvh);
     std::vector<MatRec> mrec(n_mats);
     std::vector<LightMatRec> lm(static_cast<size_t>(n_mats) * n_lights);
     for (int m = 0; m < n_mats; ++m) {
@@ -416,6 +520,8 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     ds.off_mats = off;    off += units(mrec.size() * sizeof(MatRec));
     ds.off_lights = off;  off += units(lrec.size() * sizeof(LightRec));
     ds.off_lightmat = off; off += units(lm.size() * sizeof(LightMatRec));
+    ds.off_bvh = off;     off += units(bvh.size() * sizeof(BvhNode));
+    ds.n_bvh = static_cast<int32_t>(bvh.size());
     ds.blob_units = off;
     ds.n_spheres = static_cast<int32_t>(sph.size());
     ds.n_boxes = static_cast<int32_t>(boxes.size());
@@ -431,6 +537,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     put(ds.off_mats, mrec.data(), mrec.size() * sizeof(MatRec));
     put(ds.off_lights, lrec.data(), lrec.size() * sizeof(LightRec));
     put(ds.off_lightmat, lm.data(), lm.size() * sizeof(LightMatRec));
+    put(ds.off_bvh, bvh.data(), bvh.size() * sizeof(BvhNode));
     return RT_OK;
 }
 

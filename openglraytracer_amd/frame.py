@@ -1,9 +1,10 @@
 """Row-tiled multi-GPU frame layout.
 
 A frame of H rows is cut into blocks of `block_rows` rows dealt round-robin to
-N shards (rt_render_shard renders shard s's blocks packed densely, in order).
-Interleaved blocks balance the load: the cost of a row depends on what it sees.
-Rank 0 assembles the frame after a gather of equal-size (padded) shards.
+N shards (rt_render_shard / rt_render_batch render shard s's blocks packed
+densely, in order). Interleaved blocks balance the load: the cost of a row
+depends on what it sees. Rank 0 assembles the frames after one gather of
+equal-size flat buffers (each shard's data first, then padding).
 
 Pure index bookkeeping (numpy / torch tensors); no rendering here.
 """
@@ -20,35 +21,36 @@ def padded_shard_rows(height, block_rows, n_shards):
     return max(len(shard_row_ids(height, block_rows, n_shards, s)) for s in range(n_shards))
 
 
-def gather_index(height, block_rows, n_shards):
-    """(src, dst): row src of the stacked padded shards -> frame row dst."""
-    pad = padded_shard_rows(height, block_rows, n_shards)
-    src, dst = [], []
-    for s in range(n_shards):
-        ids = shard_row_ids(height, block_rows, n_shards, s)
-        src.append(s * pad + np.arange(len(ids)))
-        dst.append(ids)
-    return np.concatenate(src), np.concatenate(dst)
+def flat_shard_elems(n_frames, height, width, block_rows, n_shards, channels=4):
+    """Elements of the equal-size flat buffer every rank contributes."""
+    return n_frames * padded_shard_rows(height, block_rows, n_shards) * width * channels
 
 
-def assemble(gathered, height, block_rows):
-    """gathered: list (one per shard) of tensors (..., pad_rows, W, C) with the
-    row axis at -3. Returns the frame (..., H, W, C) (torch or numpy)."""
-    n = len(gathered)
-    src, dst = gather_index(height, block_rows, n)
+def assembly_permutation(height, block_rows, n_shards):
+    """perm[r] = position of frame row r in the concatenation of the shards."""
+    order = np.concatenate([shard_row_ids(height, block_rows, n_shards, s) for s in range(n_shards)])
+    perm = np.empty(height, np.int64)
+    perm[order] = np.arange(height)
+    return perm
+
+
+def assemble(flat, n_frames, height, width, block_rows, channels=4, perm=None):
+    """flat: one flat buffer per shard (torch or numpy), shard s holding
+    (n_frames, rows_s, width, channels) at its start. Returns the frames
+    (n_frames, height, width, channels) in row order."""
+    n = len(flat)
+    if perm is None:
+        perm = assembly_permutation(height, block_rows, n)
+    parts = []
+    for s, buf in enumerate(flat):
+        rows = len(shard_row_ids(height, block_rows, n, s))
+        parts.append(buf[: n_frames * rows * width * channels].reshape(n_frames, rows, width, channels))
     try:
         import torch
-        if isinstance(gathered[0], torch.Tensor):
-            stacked = torch.cat(list(gathered), dim=-3)
-            out = torch.empty(stacked.shape[:-3] + (height,) + stacked.shape[-2:], dtype=stacked.dtype,
-                              device=stacked.device)
-            s_idx = torch.as_tensor(src, device=stacked.device)
-            d_idx = torch.as_tensor(dst, device=stacked.device)
-            out.index_copy_(out.dim() - 3, d_idx, stacked.index_select(stacked.dim() - 3, s_idx))
-            return out
+        if isinstance(flat[0], torch.Tensor):
+            cat = torch.cat(parts, dim=1)
+            idx = perm if isinstance(perm, torch.Tensor) else torch.as_tensor(perm, device=cat.device)
+            return cat.index_select(1, idx)
     except ImportError:
         pass
-    stacked = np.concatenate(gathered, axis=-3)
-    out = np.empty(stacked.shape[:-3] + (height,) + stacked.shape[-2:], stacked.dtype)
-    out[..., dst, :, :] = stacked[..., src, :, :]
-    return out
+    return np.concatenate(parts, axis=1)[:, perm]

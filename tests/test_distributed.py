@@ -16,6 +16,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 W, H, BLOCK, DEPTH = 64, 37, 4, 1
+TIMES = [0.0, 0.5]
+FRAMES = len(TIMES)
 
 
 def free_port():
@@ -33,14 +35,16 @@ def worker(rank, world, port, result_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     objs = scenes.bench_objects(16)
     ids = frame.shard_row_ids(H, BLOCK, world, rank)
-    pad = frame.padded_shard_rows(H, BLOCK, world)
-    shard = torch.zeros((pad, W, 4), dtype=torch.float32)
-    for i, r in enumerate(ids):
-        shard[i] = torch.from_numpy(oracle_port.render(objs, W, H, DEPTH, 0.0, rows=(int(r), int(r) + 1))[0])
-    gathered = [torch.zeros_like(shard) for _ in range(world)] if rank == 0 else None
-    dist.gather(shard, gathered, dst=0)
+    # the layout rt_render_batch writes: (frames, this shard's rows, W, 4)
+    # at the start of an equal-size flat buffer
+    buf = torch.zeros(frame.flat_shard_elems(FRAMES, H, W, BLOCK, world), dtype=torch.float32)
+    data = np.stack([np.concatenate([oracle_port.render(objs, W, H, DEPTH, t, rows=(int(r), int(r) + 1))
+                                     for r in ids]) for t in TIMES])
+    buf[: data.size] = torch.from_numpy(data.reshape(-1))
+    gathered = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gathered, dst=0)
     if rank == 0:
-        np.save(result_path, frame.assemble(gathered, H, BLOCK).numpy())
+        np.save(result_path, frame.assemble(gathered, FRAMES, H, W, BLOCK).numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -50,5 +54,5 @@ def test_gather_assembles_full_frame(tmp_path, world):
     from oracle import port as oracle_port, scenes
     out = str(tmp_path / "frame.npy")
     mp.start_processes(worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
-    full = oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, 0.0)
+    full = np.stack([oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, t) for t in TIMES])
     assert np.array_equal(np.load(out), full)

@@ -115,15 +115,34 @@ def test_shards_reassemble_the_frame(gpu_ctx, n_shards, block):
     view = rt.make_view(None, 0.0)
     sc = rt.Scene(gpu_ctx, objs)
     full = rt.render(gpu_ctx, sc, w, h, 1, view=view)
-    pad = frame.padded_shard_rows(h, block, n_shards)
+    elems = frame.flat_shard_elems(1, h, w, block, n_shards)
     shards = []
     for s in range(n_shards):
-        buf = torch.zeros((pad, w, 4), dtype=torch.float32, device="cuda")
+        buf = torch.zeros(elems, dtype=torch.float32, device="cuda")
         rt.render_shard(gpu_ctx, sc, buf.data_ptr(), w, h, 1, block, n_shards, s, view=view)
         shards.append(buf)
     torch.cuda.synchronize()
-    assembled = frame.assemble(shards, h, block).cpu().numpy()
-    assert np.array_equal(assembled, full)
+    assembled = frame.assemble(shards, 1, h, w, block).cpu().numpy()
+    assert np.array_equal(assembled[0], full)
+    sc.close()
+
+
+@pytest.mark.parametrize("n_shards", [1, 2, 8])
+def test_batched_frames_equal_single_frames(gpu_ctx, n_shards):
+    """rt_render_batch: K views in one launch == K separate renders, whole
+    frames or one shard's rows of each."""
+    objs = scenes.bench_objects(16)
+    w, h, block = 320, 180, 8
+    views = [rt.make_view(None, k / 60.0) for k in range(5)]
+    sc = rt.Scene(gpu_ctx, objs)
+    singles = [rt.render(gpu_ctx, sc, w, h, 1, view=v) for v in views]
+    for shard in range(n_shards):
+        rows = frame.shard_row_ids(h, block, n_shards, shard)
+        out = torch.zeros((len(views), len(rows), w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, 1, views, block, n_shards, shard)
+        got = out.cpu().numpy()
+        for k in range(len(views)):
+            assert np.array_equal(got[k], singles[k][rows]), (shard, k)
     sc.close()
 
 
@@ -223,3 +242,37 @@ def test_errors(gpu_ctx):
         rt.Scene(gpu_ctx, [bad])
     assert e.value.code == rt.abi.RT_ERR_INVALID
     sc.close()
+
+
+@pytest.mark.parametrize("cfg,w,h", [("config1", 128, 72), ("config2", 192, 108), ("config3", 192, 108),
+                                     ("config4", 256, 144)])
+def test_culling_and_bvh_change_nothing(gpu_ctx, cfg, w, h):
+    """RT_OPT_CULLING (screen footprints, light cones, sphere BVH, box fast
+    paths) must give bit-identical frames."""
+    build, _, _, depth = scenes.CONFIGS[cfg]
+    objs = build()
+    view = rt.make_view(None, 0.0)
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        gpu_ctx.set_culling(True)
+        on = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+        gpu_ctx.set_culling(False)
+        off = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+    finally:
+        gpu_ctx.set_culling(True)
+        sc.close()
+    assert np.array_equal(on, off, equal_nan=True)
+    o = oracle_render(objs, w, h, depth)
+    assert np.array_equal(on, o), parity_stats(on, o)
+
+
+def test_degenerate_spheres_do_not_break_the_bvh(gpu_ctx):
+    objs = scenes.bench_objects(40, seed=5)
+    objs[3].radius = float("nan")
+    objs[7].position[0] = float("inf")
+    objs[9].radius = 1e30
+    objs[11].radius = -1.5  # radius != -1: a sphere of radius 1.5 (:759)
+    view = rt.make_view(None, 0.0)
+    g = gpu_render(gpu_ctx, objs, 96, 54, 3, view)
+    o = oracle_render(objs, 96, 54, 3)
+    assert np.array_equal(g, o, equal_nan=True), parity_stats(g, o)

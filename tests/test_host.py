@@ -82,17 +82,23 @@ def test_shard_rows_partition_the_frame(h, b, n):
     assert [len(i) for i in ids] == [rt.shard_rows(h, b, n, s) for s in range(n)]
 
 
-def test_assemble_restores_row_order():
-    h, w, b, n = 37, 5, 4, 3
-    full = np.random.default_rng(0).random((2, h, w, 4)).astype(np.float32)
-    pad = frame.padded_shard_rows(h, b, n)
-    shards = []
+@pytest.mark.parametrize("torch_tensors", [False, True])
+def test_assemble_restores_row_order(torch_tensors):
+    h, w, b, n, k = 37, 5, 4, 3, 2
+    full = np.random.default_rng(0).random((k, h, w, 4)).astype(np.float32)
+    elems = frame.flat_shard_elems(k, h, w, b, n)
+    flat = []
     for s in range(n):
         ids = frame.shard_row_ids(h, b, n, s)
-        x = np.zeros((2, pad, w, 4), np.float32)
-        x[:, :len(ids)] = full[:, ids]
-        shards.append(x)
-    assert np.array_equal(frame.assemble(shards, h, b), full)
+        x = np.full(elems, np.nan, np.float32)
+        x[: k * len(ids) * w * 4] = full[:, ids].reshape(-1)
+        flat.append(x)
+    if torch_tensors:
+        import torch
+        out = frame.assemble([torch.from_numpy(x) for x in flat], k, h, w, b).numpy()
+    else:
+        out = frame.assemble(flat, k, h, w, b)
+    assert np.array_equal(out, full)
 
 
 def test_pack_rgba8_matches_gl_unorm():
