@@ -182,6 +182,20 @@ int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views
                     int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
                     void *hip_stream);
 
+/* Monte-Carlo extension (the reference has one
+ * ray per pixel): adds, for every pixel of rows [row_begin, row_end), the sum
+ * of samples [sample_offset, sample_offset + spp) — in sample order — to
+ * accum_device (float4 per pixel, caller-zeroed, device memory). Sample s of
+ * pixel (x, y) is the reference ray through NDC ((x - W/2 + jx) / (W/2),
+ * (y - H/2 + jy) / (H/2)) with (jx, jy) in [0, 1)^2 from a counter-based hash
+ * of (seed, s, y*W + x) when jitter != 0, else (0, 0) (then every sample
+ * equals the reference frame). The mean is accum / total samples. Disjoint
+ * sample ranges on several GPUs sum (RCCL all-reduce) to the same estimate
+ * up to float re-association. */
+int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width, int height,
+                         int max_depth, int spp, int sample_offset, uint32_t seed, int jitter, int row_begin,
+                         int row_end, float *accum_device, void *hip_stream);
+
 /* Context options. RT_OPT_CULLING (default 1): skip spheres that provably
  * cannot be hit (conservative footprints / light cones with margins far
  * above float error) — output is bit-identical either way. */

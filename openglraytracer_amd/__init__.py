@@ -66,6 +66,7 @@ def lib():
             "rt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i),
             "rt_context_set": ([vp, i, i], i),
             "rt_render_batch": ([vp, vp, vp, i, i, i, i, i, i, i, vp, vp], i),
+            "rt_render_accumulate": ([vp, vp, vp, i, i, i, i, i, C.c_uint32, i, i, i, vp, vp], i),
             "rt_pack_rgba8": ([vp, C.c_size_t, vp], i),
             "rt_write_ppm": ([C.c_char_p, vp, i, i], i), "rt_write_pfm": ([C.c_char_p, vp, i, i], i),
             "rt_last_error": ([], C.c_char_p), "rt_version": ([], C.c_char_p),
@@ -257,6 +258,18 @@ def render_batch(ctx, scene, out_ptr, width, height, max_depth, views, block_row
     _check(lib().rt_render_batch(ctx.handle, scene.handle, arr, len(views), width, height, max_depth,
                                  block_rows, n_shards, shard, C.c_void_p(out_ptr),
                                  C.c_void_p(stream) if stream else None))
+
+
+def render_accumulate(ctx, scene, accum_ptr, width, height, max_depth, spp, sample_offset=0, seed=0,
+                      jitter=True, view=None, rows=None, stream=None):
+    """Monte-Carlo: add the sum of samples [sample_offset, sample_offset+spp)
+    of every pixel to the float4 device accumulator at accum_ptr."""
+    r0, r1 = rows if rows is not None else (0, height)
+    if view is None:
+        view = make_view(None, 0.0)
+    _check(lib().rt_render_accumulate(ctx.handle, scene.handle, C.byref(view), width, height, max_depth, spp,
+                                      sample_offset, seed, 1 if jitter else 0, r0, r1, C.c_void_p(accum_ptr),
+                                      C.c_void_p(stream) if stream else None))
 
 
 def render_shard(ctx, scene, out_ptr, width, height, max_depth, block_rows, n_shards, shard,

@@ -329,6 +329,36 @@ int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views
     return RT_OK;
 }
 
+int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width, int height,
+                         int max_depth, int spp, int sample_offset, uint32_t seed, int jitter, int row_begin,
+                         int row_end, float *accum_device, void *hip_stream) {
+    int rc = check_render_args(ctx, scene, width, height, max_depth);
+    if (rc != RT_OK) return rc;
+    if (!view || !accum_device || spp <= 0 || sample_offset < 0 || row_begin < 0 || row_end > height ||
+        row_begin >= row_end) {
+        set_error("rt_render_accumulate: bad view / accumulator / spp / row range");
+        return RT_ERR_INVALID;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    LaunchParams p = base_params(ctx, scene, view, 1, width, height);
+    p.row_begin = row_begin;
+    p.n_rows = row_end - row_begin;
+    p.spp = spp;
+    p.sample0 = sample_offset;
+    p.seed = seed;
+    p.jitter = jitter ? 1 : 0;
+    p.out = reinterpret_cast<float4 *>(accum_device);
+    hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    rc = launch(ctx, p, max_depth, stream);
+    if (rc != RT_OK) return rc;
+    if (!hip_stream) {
+        e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail("render", e);
+    }
+    return RT_OK;
+}
+
 int rt_context_set(rt_context *ctx, int option, int value) {
     if (!ctx) { set_error("rt_context_set: null context"); return RT_ERR_INVALID; }
     switch (option) {

@@ -98,6 +98,11 @@ struct LaunchParams {
     int32_t off_spheres, off_smeta, off_boxes, off_mats, off_lights, off_lightmat;  // 16-B units
     int32_t off_bvh, n_bvh;  // sphere BVH nodes (2 x float4 each), 16-B units / count
     int32_t blob_units;      // blob size, 16-B units
+    // Monte-Carlo accumulation (render_kernel<D, true>): samples
+    // [sample0, sample0 + spp) per pixel, jittered inside the pixel when
+    // jitter != 0, summed in sample order and added to out.
+    int32_t spp, sample0, jitter;
+    uint32_t seed;
 };
 
 struct DeviceScene {

@@ -543,6 +543,10 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
             __float_as_uint(ns.x) != __float_as_uint(spe.x) || __float_as_uint(ns.y) != __float_as_uint(spe.y) ||
             __float_as_uint(ns.z) != __float_as_uint(spe.z) || __float_as_uint(ns.w) != __float_as_uint(spe.w);
         const bool need = valid && changes;
+#ifdef RT_ABLATE_SHADOW
+        if (need) { dif = nd; spe = ns; }
+        continue;
+#endif
         if (__any(need)) {
             const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sub(lpos, c.p), c.p, lpos, j, need);
             if (need && !shadowed) {
@@ -574,7 +578,11 @@ __device__ __forceinline__ v3 trace_body(const Scene &S, const Ray &r, bool vali
     const bool hit = valid && h.obj >= 0;
     if (!__any(hit)) return black;  // per-wave early out
     const Collision c = resolve(S, r, h, hit);
+#ifdef RT_ABLATE_PHONG
+    v3 col = add(c.p, c.n);
+#else
     v3 col = phong(S, r, c, hit);
+#endif
     if constexpr (kDepth > 0) {
         const MatRec &m = S.mat[c.material];
 #pragma unroll 1
@@ -648,7 +656,25 @@ __device__ int4 sphere_footprint(const LaunchParams &p, const FrameView &V, floa
     return make_int4(static_cast<int>(fx0), static_cast<int>(fx1), static_cast<int>(fy0), static_cast<int>(fy1));
 }
 
-template <int kDepth>
+// Counter-based sample jitter (Monte-Carlo extension):
+// a 32-bit integer hash of (seed, sample, pixel, axis); u in [0, 1) with 24
+// bits. Integer-only, so the oracle reproduces it exactly.
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32_t pixel, uint32_t axis) {
+    uint32_t h = mix32(seed * 0x9E3779B1u + 0x7F4A7C15u);
+    h = mix32(h ^ (sample * 0x85EBCA77u));
+    h = mix32(h ^ (pixel * 0xC2B2AE3Du + axis));
+    return static_cast<float>(h >> 8) * (1.0f / 16777216.0f);
+}
+
+template <int kDepth, bool kAccum>
 __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     // ---- stage the scene blob into LDS (one pass per work-group) ----
@@ -714,30 +740,59 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
 
     // ---- camera ray (:377-392) ----
     const int hw = p.width / 2, hh = p.height / 2;
-    const float vx = static_cast<float>(x - hw) / static_cast<float>(hw);
-    const float vy = static_cast<float>(y - hh) / static_cast<float>(hh);
     const float *M = V.unproj;  // column-major
-    float ws[4], we[4];
+    // jx, jy: sub-pixel offsets of a Monte-Carlo sample (0 for the
+    // reference's one ray per pixel; float(x - hw) + 0.0f is exact)
+    auto camera_ray = [&](float jx, float jy) {
+        const float vx = (static_cast<float>(x - hw) + jx) / static_cast<float>(hw);
+        const float vy = (static_cast<float>(y - hh) + jy) / static_cast<float>(hh);
+        float ws[4], we[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        ws[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 0.5f + M[12 + k] * 1.0f;
-        we[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 1.0f + M[12 + k] * 1.0f;
-    }
-    const v3 s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
-    const v3 e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
-    Ray ray;
-    ray.start = origin;
-    ray.dir = normalize(sub(e3, s3));
-
-    const v3 col = trace<kDepth, true>(S, ray, active);
+        for (int k = 0; k < 4; ++k) {
+            ws[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 0.5f + M[12 + k] * 1.0f;
+            we[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 1.0f + M[12 + k] * 1.0f;
+        }
+        const v3 s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
+        const v3 e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
+        Ray ray;
+        ray.start = origin;
+        ray.dir = normalize(sub(e3, s3));
+        return ray;
+    };
     float4 *out = p.out + static_cast<size_t>(blockIdx.z) * p.n_rows * p.width;
-    if (active) out[static_cast<size_t>(local_row) * p.width + x] = make_float4(col.x, col.y, col.z, 0.0f);
+    const size_t idx = static_cast<size_t>(local_row) * p.width + x;
+
+    if constexpr (!kAccum) {
+        const Ray ray = camera_ray(0.0f, 0.0f);
+#ifdef RT_ABLATE_TRACE
+        const v3 col = ray.dir;
+#else
+        const v3 col = trace<kDepth, true>(S, ray, active);
+#endif
+        if (active) out[idx] = make_float4(col.x, col.y, col.z, 0.0f);
+    } else {
+        const uint32_t pixel = static_cast<uint32_t>(y) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x);
+        v3 acc = mk(0.0f, 0.0f, 0.0f);
+        for (int smp = 0; smp < p.spp; ++smp) {
+            const uint32_t sid = static_cast<uint32_t>(p.sample0 + smp);
+            const float jx = p.jitter ? jitter_u(p.seed, sid, pixel, 0u) : 0.0f;
+            const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
+            acc = add(acc, trace<kDepth, true>(S, camera_ray(jx, jy), active));
+        }
+        if (active) {
+            const float4 o = out[idx];
+            out[idx] = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + 0.0f);
+        }
+    }
 }
 
 template <int kDepth>
 hipError_t launch_depth(const LaunchParams &p, hipStream_t stream) {
     const dim3 grid((p.width + kTile - 1) / kTile, (p.n_rows + kTile - 1) / kTile, p.n_views);
-    hipLaunchKernelGGL(render_kernel<kDepth>, grid, dim3(kThreads), lds_bytes(p), stream, p);
+    if (p.spp > 0)
+        hipLaunchKernelGGL((render_kernel<kDepth, true>), grid, dim3(kThreads), lds_bytes(p), stream, p);
+    else
+        hipLaunchKernelGGL((render_kernel<kDepth, false>), grid, dim3(kThreads), lds_bytes(p), stream, p);
     return hipGetLastError();
 }
 
@@ -768,12 +823,11 @@ hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t strea
 // (gfx950 has 160 KiB per CU). Best effort: a failure only lowers the largest
 // scene that fits, which rt_scene_create checks.
 hipError_t allow_large_lds(size_t bytes) {
-    const void *fns[] = {
-        reinterpret_cast<const void *>(&render_kernel<0>), reinterpret_cast<const void *>(&render_kernel<1>),
-        reinterpret_cast<const void *>(&render_kernel<2>), reinterpret_cast<const void *>(&render_kernel<3>),
-        reinterpret_cast<const void *>(&render_kernel<4>), reinterpret_cast<const void *>(&render_kernel<5>),
-        reinterpret_cast<const void *>(&render_kernel<6>), reinterpret_cast<const void *>(&render_kernel<7>),
-        reinterpret_cast<const void *>(&render_kernel<8>), reinterpret_cast<const void *>(&render_kernel<9>)};
+#define RT_KFN(d) reinterpret_cast<const void *>(&render_kernel<d, false>), \
+                  reinterpret_cast<const void *>(&render_kernel<d, true>)
+    const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
+                         RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9)};
+#undef RT_KFN
     for (const void *f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
     (void)hipGetLastError();  // do not leak a sticky error into the next launch check

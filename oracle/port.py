@@ -73,3 +73,28 @@ def render(objects, width, height, max_depth=0, time=0.0, rows=None, probe=0, ma
     if rc != 0:
         raise ValueError("oracle_render rejected its arguments")
     return out
+
+
+def render_accumulate(objects, width, height, max_depth, spp, sample0=0, seed=0, jitter=True, accum=None,
+                      time=0.0, rows=None, materials=None, lights=None, camera=None, threads=0):
+    """Checker of rt_render_accumulate: adds the in-order sample sums to `accum`
+    ((r1-r0, width, 4) float32, zeros if None) and returns it."""
+    materials = materials if materials is not None else reference_materials()
+    lights = lights if lights is not None else reference_lights()
+    r0, r1 = rows if rows is not None else (0, height)
+    objs = (Object * max(len(objects), 1))(*objects)
+    mats = (Material * len(materials))(*materials)
+    lts = (Light * max(len(lights), 1))(*lights)
+    if accum is None:
+        accum = np.zeros((r1 - r0, width, 4), np.float32)
+    cam = C.byref(camera) if camera is not None else None
+    L = lib()
+    L.oracle_render_accumulate.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                           C.c_void_p, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    rc = L.oracle_render_accumulate(C.addressof(objs), len(objects), C.addressof(mats), len(materials),
+                                    C.addressof(lts), len(lights), cam, C.c_float(time), width, height, max_depth,
+                                    spp, sample0, seed, 1 if jitter else 0, r0, r1, threads, accum.ctypes.data)
+    if rc != 0:
+        raise ValueError("oracle_render_accumulate rejected its arguments")
+    return accum

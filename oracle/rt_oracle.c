@@ -696,6 +696,87 @@ static v3 recursive_raytrace(const scene_t *S, machine_t *M, ray_t r, int max_de
     return M->popped.final_color;
 }
 
+/* Monte-Carlo extension: the same counter-based jitter hash as the kernel. */
+static uint32_t mix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+    return h;
+}
+static float jitter_u(uint32_t seed, uint32_t sample, uint32_t pixel, uint32_t axis) {
+    uint32_t h = mix32(seed * 0x9E3779B1u + 0x7F4A7C15u);
+    h = mix32(h ^ (sample * 0x85EBCA77u));
+    h = mix32(h ^ (pixel * 0xC2B2AE3Du + axis));
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+/* :377-392 with optional sub-pixel offsets (0 = the reference's ray). */
+static ray_t camera_ray(m4 inv, const rt_camera *cam, int x, int y, int hw, int hh, float jx, float jy) {
+    float vx = ((float)(x - hw) + jx) / (float)hw;
+    float vy = ((float)(y - hh) + jy) / (float)hh;
+    v4 ws = mul4v(inv, V4(vx, vy, 0.5f, 1.0f));
+    ws = V4(ws.x / ws.w, ws.y / ws.w, ws.z / ws.w, ws.w / ws.w);
+    v4 we = mul4v(inv, V4(vx, vy, 1.0f, 1.0f));
+    we = V4(we.x / we.w, we.y / we.w, we.z / we.w, we.w / we.w);
+    ray_t r;
+    r.start = ld3(cam->position);
+    r.dir = normalize3(V3(we.x - ws.x, we.y - ws.y, we.z - ws.z));
+    return r;
+}
+
+static obj_t *prepare_objects(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats) {
+    obj_t *o = (obj_t *)calloc((size_t)(n_objs > 0 ? n_objs : 1), sizeof(obj_t));
+    for (int i = 0; i < n_objs; i++) {
+        const rt_object *s = &objs[i];
+        int is_box = !(s->box_mins[0] == 0.0f && s->box_mins[1] == 0.0f && s->box_mins[2] == 0.0f &&
+                       s->box_maxs[0] == 0.0f && s->box_maxs[1] == 0.0f && s->box_maxs[2] == 0.0f);
+        o[i].kind = is_box ? 1 : (s->radius != -1.0f ? 2 : 0);
+        if (s->material < 0 || s->material >= n_mats) { free(o); return NULL; }
+        o[i].mat = &mats[s->material];
+        o[i].mins = ld3(s->box_mins); o[i].maxs = ld3(s->box_maxs);
+        o[i].pos = ld3(s->position); o[i].radius = s->radius;
+        object_transforms(o[i].pos, ld3(s->angles), &o[i].l2w, &o[i].w2l, &o[i].nrm);
+    }
+    return o;
+}
+
+/* Monte-Carlo accumulation (see rt_render_accumulate in include/rt.h):
+ * accum[(y-row0)*W + x] += sum over samples s in order of the colour. */
+int oracle_render_accumulate(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats,
+                             const rt_light *lights, int n_lights, const rt_camera *cam_in, float time, int width,
+                             int height, int max_depth, int spp, int sample0, uint32_t seed, int jitter, int row0,
+                             int row1, int n_threads, float *accum) {
+    if (!objs || n_objs < 0 || !mats || n_mats <= 0 || (n_lights > 0 && !lights) || n_lights < 0 || width <= 0 ||
+        height <= 0 || row0 < 0 || row1 > height || row0 > row1 || max_depth < 0 || spp <= 0 || !accum)
+        return -1;
+    obj_t *o = prepare_objects(objs, n_objs, mats, n_mats);
+    if (!o) return -1;
+    scene_t S = {o, n_objs, lights, n_lights};
+    rt_camera cam;
+    if (cam_in) cam = *cam_in;
+    else oracle_reference_camera(time, &cam);
+    m4 inv = camera_unprojection(&cam);
+    int hw = width / 2, hh = height / 2;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : omp_get_max_threads())
+    for (int yy = 0; yy < row1 - row0; yy++) {
+        machine_t *M = (machine_t *)malloc(sizeof(machine_t));
+        int y = row0 + yy;
+        for (int x = 0; x < width; x++) {
+            uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
+            v3 acc = V3(0, 0, 0);
+            for (int s = 0; s < spp; s++) {
+                uint32_t sid = (uint32_t)(sample0 + s);
+                float jx = jitter ? jitter_u(seed, sid, pixel, 0u) : 0.0f;
+                float jy = jitter ? jitter_u(seed, sid, pixel, 1u) : 0.0f;
+                acc = add3(acc, recursive_raytrace(&S, M, camera_ray(inv, &cam, x, y, hw, hh, jx, jy), max_depth));
+            }
+            float *px = accum + ((size_t)yy * width + x) * 4;
+            px[0] = px[0] + acc.x; px[1] = px[1] + acc.y; px[2] = px[2] + acc.z; px[3] = px[3] + 0.0f;
+        }
+        free(M);
+    }
+    free(o);
+    return 0;
+}
+
 /* :325-405 */
 int oracle_render(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats,
                   const rt_light *lights, int n_lights, const rt_camera *cam_in, float time, int width,
@@ -703,18 +784,8 @@ int oracle_render(const rt_object *objs, int n_objs, const rt_material *mats, in
     if (!objs || n_objs < 0 || !mats || n_mats <= 0 || (n_lights > 0 && !lights) || n_lights < 0 || width <= 0 ||
         height <= 0 || row0 < 0 || row1 > height || row0 > row1 || max_depth < 0 || !out)
         return -1;
-    obj_t *o = (obj_t *)calloc((size_t)(n_objs > 0 ? n_objs : 1), sizeof(obj_t));
-    for (int i = 0; i < n_objs; i++) {
-        const rt_object *s = &objs[i];
-        int is_box = !(s->box_mins[0] == 0.0f && s->box_mins[1] == 0.0f && s->box_mins[2] == 0.0f &&
-                       s->box_maxs[0] == 0.0f && s->box_maxs[1] == 0.0f && s->box_maxs[2] == 0.0f);
-        o[i].kind = is_box ? 1 : (s->radius != -1.0f ? 2 : 0);
-        if (s->material < 0 || s->material >= n_mats) { free(o); return -1; }
-        o[i].mat = &mats[s->material];
-        o[i].mins = ld3(s->box_mins); o[i].maxs = ld3(s->box_maxs);
-        o[i].pos = ld3(s->position); o[i].radius = s->radius;
-        object_transforms(o[i].pos, ld3(s->angles), &o[i].l2w, &o[i].w2l, &o[i].nrm);
-    }
+    obj_t *o = prepare_objects(objs, n_objs, mats, n_mats);
+    if (!o) return -1;
     scene_t S = {o, n_objs, lights, n_lights};
     rt_camera cam;
     if (cam_in) cam = *cam_in;
@@ -727,15 +798,7 @@ int oracle_render(const rt_object *objs, int n_objs, const rt_material *mats, in
         machine_t *M = (machine_t *)malloc(sizeof(machine_t));
         int y = row0 + yy;
         for (int x = 0; x < width; x++) {
-            float vx = (float)(x - hw) / (float)hw;
-            float vy = (float)(y - hh) / (float)hh;
-            v4 ws = mul4v(inv, V4(vx, vy, 0.5f, 1.0f));
-            ws = V4(ws.x / ws.w, ws.y / ws.w, ws.z / ws.w, ws.w / ws.w);
-            v4 we = mul4v(inv, V4(vx, vy, 1.0f, 1.0f));
-            we = V4(we.x / we.w, we.y / we.w, we.z / we.w, we.w / we.w);
-            ray_t r;
-            r.start = ld3(cam.position);
-            r.dir = normalize3(V3(we.x - ws.x, we.y - ws.y, we.z - ws.z));
+            ray_t r = camera_ray(inv, &cam, x, y, hw, hh, 0.0f, 0.0f);
             v3 col;
             if (probe == 0) {
                 col = recursive_raytrace(&S, M, r, max_depth);

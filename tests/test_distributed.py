@@ -56,3 +56,32 @@ def test_gather_assembles_full_frame(tmp_path, world):
     mp.start_processes(worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
     full = np.stack([oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, t) for t in TIMES])
     assert np.array_equal(np.load(out), full)
+
+
+def mc_worker(rank, world, port, result_path):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import port as oracle_port, scenes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    spp_total, w, h = 8, 24, 14
+    per = spp_total // world
+    acc = oracle_port.render_accumulate(scenes.bench_objects(16), w, h, 0, per, rank * per, seed=3)
+    t = torch.from_numpy(acc)
+    dist.all_reduce(t)  # the RCCL all-reduce of config 5, here over gloo
+    if rank == 0:
+        np.save(result_path, (t / spp_total).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_monte_carlo_sample_sharding(tmp_path, world):
+    """Config 5: samples sharded over ranks + all-reduce == one rank's
+    estimate up to float re-association of the partial sums."""
+    from oracle import port as oracle_port, scenes
+    out = str(tmp_path / "mc.npy")
+    mp.start_processes(mc_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
+    ref = oracle_port.render_accumulate(scenes.bench_objects(16), 24, 14, 0, 8, 0, seed=3) / 8
+    got = np.load(out)
+    assert np.allclose(got, ref, rtol=1e-6, atol=1e-6)
