@@ -1,8 +1,8 @@
 """Benchmark: primary rays/s of the MI355X ray tracer on BASELINE.json's config.
 
-Workload (BASELINE.json configs[1]): 1920x1080,
-room box + 16 seeded spheres, the reference's 3 lights and 7 materials,
-max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
+Default workload (BASELINE.json configs[1]):
+1920x1080, room box + 16 seeded spheres, the reference's 3 lights and 7
+materials, max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
 
 A step renders N frames of 1920x1080 (N = number of GPUs; frame k is the
 reference orbit camera at time k/60 s). Every frame is row-tiled across the N
@@ -12,13 +12,19 @@ one RCCL gather over xGMI plus a row de-interleave. Per-GPU work is one frame
 per step at every N: weak scaling. At N=1 a step is one full frame rendered
 in place (no collective).
 
-value = primary rays of all frames / step time (max over ranks), Mrays/s.
+--workload config5 (a Monte-Carlo extension the
+reference does not have): one step = the 1920x1080 frame at 1024 jittered
+samples per pixel, samples sharded over the N ranks, partial sums combined
+with one RCCL all-reduce: strong scaling; value = samples/s.
+
+value = primary rays (samples) of the step / step time (max over ranks), Mrays/s.
 roofline = the render kernel against the HBM-write roofline: 16 B per pixel
-(one float4 store) / average kernel time from HIP events on the launch stream.
+(one float4 store) / average kernel time from HIP events around every launch
+of the timed region, on the launch stream.
 cpu_baseline = the reference's own shader on Mesa llvmpipe (oracle/_ref) over a
 bounded band of the same frame, in a child process on the host cores.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config5]
 """
 import argparse
 import json
@@ -34,6 +40,7 @@ sys.path.insert(0, ROOT)
 
 WIDTH, HEIGHT, N_SPHERES, MAX_DEPTH = 1920, 1080, 16, 0
 BLOCK_ROWS = 8
+MC_SPP = 1024
 BYTES_PER_PIXEL = 16  # one float4 store per pixel (algorithmic HBM bytes)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "primary Mrays/s at 1920×1080; achieved HBM GB/s vs peak; 1/2/4/8-GPU scaling"
@@ -44,6 +51,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["config2", "config5"], default="config2")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="approximate budget of the llvmpipe baseline sample")
@@ -69,14 +79,14 @@ def cpu_baseline(budget_s):
     return None
 
 
-def pmc_traffic():
+def pmc_traffic(workload):
     """Per-launch HBM bytes of the render kernel from the committed PMC pass
     (profiles/pmc_latest.json, written by tools/pmc_summary.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == "config2" and d.get("n_gpus", 1) == 1:
+        if d.get("workload") == workload and d.get("n_gpus", 1) == 1:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -96,24 +106,42 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
-    torch.cuda.set_device(local)
+    device = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
+    coll_dev = "cuda"
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.dist_backend)
+            coll_dev = "cpu"
 
-    ctx = rt.Context(local)
+    ctx = rt.Context(device)
     scene = rt.Scene(ctx, rt.bench_objects(N_SPHERES, 0))
-    n_frames = world
-    views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
+    mc = args.workload == "config5"
 
-    # every launch renders this rank's rows of all n_frames frames
-    # (rt_render_batch: blockIdx.z = frame); N=1 renders whole frames in place
-    rows_mine = HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
-    flat_elems = frame.flat_shard_elems(n_frames, HEIGHT, WIDTH, BLOCK_ROWS, world)
-    buf = torch.zeros(flat_elems, dtype=torch.float32, device="cuda")
-    gathered = [torch.empty_like(buf) for _ in range(world)] if (world > 1 and rank == 0) else None
-    perm = torch.as_tensor(frame.assembly_permutation(HEIGHT, BLOCK_ROWS, world), device="cuda")
+    if not mc:
+        n_frames = world
+        views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
+        # every launch renders this rank's rows of all n_frames frames
+        # (rt_render_batch: blockIdx.z = frame); N=1 renders whole frames in place
+        rows_mine = HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
+        flat_elems = frame.flat_shard_elems(n_frames, HEIGHT, WIDTH, BLOCK_ROWS, world)
+        buf = torch.zeros(flat_elems, dtype=torch.float32, device="cuda")
+        gathered = ([torch.empty(flat_elems, dtype=torch.float32, device=coll_dev) for _ in range(world)]
+                    if (world > 1 and rank == 0) else None)
+        perm = torch.as_tensor(frame.assembly_permutation(HEIGHT, BLOCK_ROWS, world), device=coll_dev)
+        px_per_launch = WIDTH * rows_mine * n_frames
+        rays_per_step = n_frames * WIDTH * HEIGHT
+    else:
+        view = rt.make_view(None, 0.0)
+        spp_mine = MC_SPP // world + (1 if rank < MC_SPP % world else 0)
+        sample0 = rank * (MC_SPP // world) + min(rank, MC_SPP % world)
+        accum = torch.zeros((HEIGHT, WIDTH, 4), dtype=torch.float32, device="cuda")
+        px_per_launch = WIDTH * HEIGHT
+        rays_per_step = MC_SPP * WIDTH * HEIGHT
 
     # HIP events around every render launch of the timed region, on the
     # stream the kernel is launched on
@@ -123,14 +151,27 @@ def main():
     def step(timed, it=0):
         if timed:
             ev[it][0].record(stream)
-        rt.render_batch(ctx, scene, buf.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS,
-                        world, rank, stream=sh)
+        if not mc:
+            rt.render_batch(ctx, scene, buf.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS,
+                            world, rank, stream=sh)
+        else:
+            accum.zero_()
+            rt.render_accumulate(ctx, scene, accum.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, spp_mine, sample0,
+                                 seed=0, view=view, stream=sh)
         if timed:
             ev[it][1].record(stream)
-        if world > 1:
-            dist.gather(buf, gathered, dst=0)
-            if rank == 0:  # (n_frames, H, W, 4) in frame row order
-                frame.assemble(gathered, n_frames, HEIGHT, WIDTH, BLOCK_ROWS, perm=perm)
+        if not mc:
+            if world > 1:
+                dist.gather(buf if coll_dev == "cuda" else buf.cpu(), gathered, dst=0)
+                if rank == 0:  # (n_frames, H, W, 4) in frame row order
+                    frame.assemble(gathered, n_frames, HEIGHT, WIDTH, BLOCK_ROWS, perm=perm)
+        else:
+            total = accum
+            if world > 1:
+                total = accum if coll_dev == "cuda" else accum.cpu()
+                dist.all_reduce(total)
+            if rank == 0:
+                total.mul_(1.0 / MC_SPP)  # the estimate: mean over all samples
 
     for _ in range(args.warmup):
         step(False)
@@ -148,20 +189,29 @@ def main():
     elapsed = t1 - t0
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
-    rays = n_frames * WIDTH * HEIGHT * args.steps
-    value = rays / elapsed / 1e6
+    value = rays_per_step * args.steps / elapsed / 1e6
     avg_kernel_ms = float(np.mean(kernel_ms))
-    px_per_launch = WIDTH * rows_mine * n_frames
     achieved = px_per_launch * BYTES_PER_PIXEL / (avg_kernel_ms * 1e-3) / 1e9
-    traffic = pmc_traffic() if world == 1 else None
+    traffic = pmc_traffic(args.workload) if world == 1 else None
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not mc:
             cpu = cpu_baseline(args.cpu_seconds)
+        if not mc:
+            workload = {"workload": "config2: 1920x1080, room box + 16 spheres, max_depth 0 "
+                                    "(primary + shadow rays)",
+                        "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES, "max_depth": MAX_DEPTH,
+                        "frames_per_step": n_frames, "row_block": BLOCK_ROWS,
+                        "parallelism": ("row-tiles x%d + RCCL gather" % world) if world > 1 else "single GPU"}
+        else:
+            workload = {"workload": "config5: 1920x1080 x 1024 spp Monte-Carlo, room box + 16 spheres, "
+                                    "max_depth 0", "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES,
+                        "spp": MC_SPP, "max_depth": MAX_DEPTH,
+                        "parallelism": ("samples x%d + RCCL all-reduce" % world) if world > 1 else "single GPU"}
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -171,15 +221,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if mc else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded scene, SURVEY.md §8(d) config 2)",
-            "config": {"workload": "config2: 1920x1080, room box + 16 spheres, max_depth 0 "
-                                   "(primary + shadow rays)",
-                       "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES, "max_depth": MAX_DEPTH,
-                       "frames_per_step": n_frames, "row_block": BLOCK_ROWS,
-                       "parallelism": "row-tiles x%d + RCCL gather" % world if world > 1 else "single GPU"},
+            "data": "synthetic (seeded scene, SURVEY.md §8(d) %s)" % args.workload,
+            "config": workload,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
