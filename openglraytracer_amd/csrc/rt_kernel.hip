@@ -428,6 +428,28 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     const float maxlen = wave_max(act ? ul : 0.0f);
     const float al = dot(ax, ax);
     const bool angular = cmin > 0.0f && al > 0.5f;  // cone narrower than 90 degrees, axis a unit vector
+    if (!angular && S.nbvh > 0) {
+        // incoherent shadow rays (no useful common cone): per-lane any-hit
+        // walk of the sphere BVH over the segment t in (0, 1)
+        const RayInv q = ray_inv({start, dir});
+        int node = act ? 0 : -1;
+        while (node >= 0) {
+            const float4 lo = S.bvh[2 * node], hi = S.bvh[2 * node + 1];
+            const int leaf = __float_as_int(hi.w);
+            if (node_hit(q, lo, hi, 1.0f)) {
+                if (leaf) {
+                    const int first = leaf & 0xFFFFFF, count = leaf >> 24;
+                    for (int s = first; s < first + count; ++s) exact(s);
+                    node = hit ? -1 : __float_as_int(lo.w);
+                } else {
+                    node = node + 1;
+                }
+            } else {
+                node = __float_as_int(lo.w);
+            }
+        }
+        return hit;
+    }
     const float sth = __builtin_sqrtf(fmaxf(0.0f, 1.0f - cmin * cmin));
     const int lane = threadIdx.x & 63;
     for (int base = 0; base < S.ns; base += 64) {
@@ -563,60 +585,128 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
     return mk(px * pw, py * pw, pz * pw);
 }
 
-// recursive_raytrace (:1071-1105) as real recursion on a compile-time depth:
-// the stack machine's order (reflection subtree, then refraction subtree,
-// then mix(mix(phong, R, refl), T, transp)), its spawn flags (:994, :1027) and
-// "a missed ray is black" (:962-963). Lanes that do not trace a ray at this
-// level ride along with valid = false.
-template <int kDepth, bool kPrimary>
-__device__ v3 trace(const Scene &S, const Ray &r, bool valid);
-
-template <int kDepth, bool kPrimary>
-__device__ __forceinline__ v3 trace_body(const Scene &S, const Ray &r, bool valid) {
+// ---- recursive_raytrace (:1071-1105) -----------------------------------
+// The stack machine (:848-1065) evaluates, per ray: closest hit; Phong; if
+// depth remains, the reflection subtree, then the refraction subtree; then
+// mix(mix(phong, R, reflectivity), T, transparency), with a missed ray black
+// (:962-963) and each mix only when that child was spawned (:994, :1027).
+//
+// Depth 0 is one ray (trace0). Deeper trees run as an explicit depth-first
+// walk (trace_tree): every loop iteration traces ONE ray per lane — all lanes
+// execute the same closest-hit + shading code whatever their position in
+// their own tree — and per-level frames (partial colour, pending refraction
+// ray, weights) live in registers. Lanes whose tree is finished ride along
+// with valid = false.
+__device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
-    const Hit h = closest<kPrimary>(S, r, valid);
+    const Hit h = closest<true>(S, r, valid);
     const bool hit = valid && h.obj >= 0;
     if (!__any(hit)) return black;  // per-wave early out
     const Collision c = resolve(S, r, h, hit);
 #ifdef RT_ABLATE_PHONG
-    v3 col = add(c.p, c.n);
+    const v3 col = add(c.p, c.n);
 #else
-    v3 col = phong(S, r, c, hit);
+    const v3 col = phong(S, r, c, hit);
 #endif
-    if constexpr (kDepth > 0) {
-        const MatRec &m = S.mat[c.material];
-#pragma unroll 1
-        for (int k = 0; k < 2; ++k) {
-            const float w = k == 0 ? m.reflectivity : m.transparency;
-            const bool spawn = hit && w > 0.0f;
-            if (__any(spawn)) {
-                Ray cr;
-                if (k == 0) {
-                    cr.start = add(c.p, muls(c.n, 0.001f));
-                    cr.dir = reflect(r.dir, c.n);
-                } else {
-                    cr.start = sub(c.p, muls(c.n, 0.001f));
-                    float ratio = 1.0f / m.refraction_index;
-                    if (c.inside) ratio = 1.0f / ratio;
-                    cr.dir = refract(r.dir, c.n, ratio);
-                }
-                const v3 cc = trace<kDepth - 1, false>(S, cr, spawn);
-                if (spawn) col = mix(col, cc, w);
-            }
-        }
-    }
     return sel(hit, col, black);
 }
 
-template <int kDepth, bool kPrimary>
-__device__ __noinline__ v3 trace_call(const Scene &S, const Ray &r, bool valid) {
-    return trace_body<kDepth, kPrimary>(S, r, valid);
-}
+struct Frame {
+    v3 col;       // phong, then mix(phong, R, rho) once the reflection returned
+    v3 rs, rd;    // pending refraction ray (:1010-1023)
+    float rho, tau;
+    int flags;    // 1: refraction spawned; 2: waiting for the reflection; 4: for the refraction
+};
 
-template <int kDepth, bool kPrimary>
-__device__ __forceinline__ v3 trace(const Scene &S, const Ray &r, bool valid) {
-    if constexpr (kPrimary || kDepth == 0) return trace_body<kDepth, kPrimary>(S, r, valid);
-    else return trace_call<kDepth, kPrimary>(S, r, valid);
+template <int N>
+struct Frames {  // register-resident: every access uses a compile-time index
+    Frame f[N];
+    __device__ __forceinline__ Frame get(int level) const {
+        Frame r = f[0];
+#pragma unroll
+        for (int i = 1; i < N; ++i)
+            if (level == i) r = f[i];
+        return r;
+    }
+    __device__ __forceinline__ void set(int level, const Frame &v) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (level == i) f[i] = v;
+    }
+};
+
+template <int kDepth>
+__device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
+    const v3 black = mk(0.0f, 0.0f, 0.0f);
+    Frames<kDepth> F;
+    int level = 0;
+    bool done = !active;
+    v3 result = black;
+    bool first = true;
+    while (__any(!done)) {
+        const bool valid = !done;
+        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
+        first = false;
+        const bool hit = valid && h.obj >= 0;
+        const Collision c = resolve(S, ray, h, hit);
+#ifdef RT_ABLATE_PHONG
+        const v3 col = add(c.p, c.n);
+#else
+        const v3 col = phong(S, ray, c, hit);
+#endif
+        if (!valid) continue;
+        const MatRec &m = S.mat[c.material];
+        const bool sr = hit && level < kDepth && m.reflectivity > 0.0f;
+        const bool st = hit && level < kDepth && m.transparency > 0.0f;
+        if (sr || st) {  // push this node, descend into its first child
+            Frame fr;
+            fr.col = col;
+            fr.rho = m.reflectivity;
+            fr.tau = m.transparency;
+            fr.rs = sub(c.p, muls(c.n, 0.001f));
+            float ratio = 1.0f / m.refraction_index;
+            if (c.inside) ratio = 1.0f / ratio;
+            fr.rd = refract(ray.dir, c.n, ratio);
+            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4);
+            F.set(level, fr);
+            if (sr) {
+                ray.start = add(c.p, muls(c.n, 0.001f));
+                ray.dir = reflect(ray.dir, c.n);
+            } else {
+                ray.start = fr.rs;
+                ray.dir = fr.rd;
+            }
+            ++level;
+            continue;
+        }
+        // this node is finished: fold its colour into its ancestors
+        v3 value = hit ? col : black;
+        bool next_child = false;
+        while (level > 0 && !next_child) {
+            Frame fr = F.get(level - 1);
+            if (fr.flags & 2) {
+                fr.col = mix(fr.col, value, fr.rho);
+                if (fr.flags & 1) {  // the refraction child comes next
+                    fr.flags = 4;
+                    F.set(level - 1, fr);
+                    ray.start = fr.rs;
+                    ray.dir = fr.rd;
+                    next_child = true;
+                } else {
+                    value = fr.col;
+                    --level;
+                }
+            } else {
+                value = mix(fr.col, value, fr.tau);
+                --level;
+            }
+        }
+        if (!next_child) {
+            result = value;
+            done = true;
+        }
+    }
+    return result;
 }
 
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
@@ -767,7 +857,9 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
 #ifdef RT_ABLATE_TRACE
         const v3 col = ray.dir;
 #else
-        const v3 col = trace<kDepth, true>(S, ray, active);
+        v3 col;
+        if constexpr (kDepth == 0) col = trace0(S, ray, active);
+        else col = trace_tree<kDepth>(S, ray, active);
 #endif
         if (active) out[idx] = make_float4(col.x, col.y, col.z, 0.0f);
     } else {
@@ -777,7 +869,10 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
             const uint32_t sid = static_cast<uint32_t>(p.sample0 + smp);
             const float jx = p.jitter ? jitter_u(p.seed, sid, pixel, 0u) : 0.0f;
             const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
-            acc = add(acc, trace<kDepth, true>(S, camera_ray(jx, jy), active));
+            v3 col;
+            if constexpr (kDepth == 0) col = trace0(S, camera_ray(jx, jy), active);
+            else col = trace_tree<kDepth>(S, camera_ray(jx, jy), active);
+            acc = add(acc, col);
         }
         if (active) {
             const float4 o = out[idx];
