@@ -554,7 +554,12 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         const float cos_phi = dot(view, lref);
         const LightMatRec &q = S.lm[c.material * S.nl + j];
         const float kd = gmax(cos_theta, 0.0f);
-        const float ks = glsl_pow(gmax(cos_phi, 0.0f), m.shininess);
+        // pow(0, s) is +0 for s > 0 (log2 = -inf, exp2 clamps to 2^-127
+        // scaled to 0): skip the polynomials when no lane needs them
+        const float xs = gmax(cos_phi, 0.0f);
+        const bool need_pow = !(xs == 0.0f && m.shininess > 0.0f);
+        float ks = 0.0f;
+        if (__any(need_pow && valid)) ks = need_pow ? glsl_pow(xs, m.shininess) : 0.0f;
         const float4 nd = make_float4(dif.x + q.ld_md[0] * kd, dif.y + q.ld_md[1] * kd, dif.z + q.ld_md[2] * kd,
                                       dif.w + q.ld_md[3] * kd);
         const float4 ns = make_float4(spe.x + q.ls_ms[0] * ks, spe.y + q.ls_ms[1] * ks, spe.z + q.ls_ms[2] * ks,
