@@ -146,6 +146,13 @@ void rt_destroy(rt_context *ctx);
 int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt_material *mats,
                     int n_mats, const rt_light *lights, int n_lights, rt_scene **out);
 void rt_scene_destroy(rt_scene *scene);
+/* Replace the scene's contents in place (an animated frame: the reference
+ * recomputes its objects from `time` every frame, raytrace_compute.glsl:
+ * 277-307); reallocates only if the new scene is larger. Waits for renders
+ * queued on the context's own stream; renders on caller streams that read
+ * the scene must be complete. */
+int rt_scene_update(rt_context *ctx, rt_scene *scene, const rt_object *objs, int n_objs, const rt_material *mats,
+                    int n_mats, const rt_light *lights, int n_lights);
 
 /* Render rows [row_begin, row_end) of a width x height frame.
  *  cam        NULL = the reference orbit camera at `time` (main(), :334-364).

@@ -59,6 +59,7 @@ def lib():
             "rt_bench_objects": ([i, C.c_uint64, vp], i), "rt_make_view": ([vp, f, vp], i),
             "rt_create": ([i, vp], i), "rt_destroy": ([vp], None),
             "rt_scene_create": ([vp, vp, i, vp, i, vp, i, vp], i), "rt_scene_destroy": ([vp], None),
+            "rt_scene_update": ([vp, vp, vp, i, vp, i, vp, i], i),
             "rt_render": ([vp, vp, vp, f, i, i, i, i, i, vp, i, vp], i),
             "rt_render_view": ([vp, vp, vp, i, i, i, i, i, vp, i, vp], i),
             "rt_shard_rows": ([i, i, i, i], i),
@@ -209,6 +210,16 @@ class Scene:
         _check(lib().rt_scene_create(ctx.handle, objs, len(objects), mats, len(materials), lts,
                                      len(lights), C.byref(self._h)))
         self.ctx = ctx
+
+    def update(self, objects, materials=None, lights=None):
+        """Replace the contents (rt_scene_update), e.g. the next animation frame."""
+        materials = materials if materials is not None else reference_materials()
+        lights = lights if lights is not None else reference_lights()
+        objs = (Object * max(len(objects), 1))(*objects)
+        mats = (Material * len(materials))(*materials)
+        lts = (Light * max(len(lights), 1))(*lights)
+        _check(lib().rt_scene_update(self.ctx.handle, self._h, objs, len(objects), mats, len(materials), lts,
+                                     len(lights)))
 
     def close(self):
         if self._h:

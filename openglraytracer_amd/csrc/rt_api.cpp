@@ -187,7 +187,49 @@ int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt
     }
     s->device = ctx->device;
     s->dev = ds;
+    s->capacity_units = ds.blob_units > 0 ? ds.blob_units : 1;
     *out = s;
+    return RT_OK;
+}
+
+int rt_scene_update(rt_context *ctx, rt_scene *scene, const rt_object *objs, int n_objs, const rt_material *mats,
+                    int n_mats, const rt_light *lights, int n_lights) {
+    if (!ctx || !scene || scene->device != ctx->device || (n_objs > 0 && !objs) || n_objs < 0 ||
+        n_objs > RT_MAX_OBJECTS || !mats || n_mats <= 0 || n_mats > RT_MAX_MATERIALS || n_lights < 0 ||
+        n_lights > RT_MAX_LIGHTS || (n_lights > 0 && !lights)) {
+        set_error("rt_scene_update: bad arguments");
+        return RT_ERR_INVALID;
+    }
+    std::vector<float4> blob;
+    DeviceScene ds;
+    int rc = build_scene(objs, n_objs, mats, n_mats, lights, n_lights, blob, ds);
+    if (rc != RT_OK) return rc;
+    LaunchParams probe{};
+    probe.blob_units = ds.blob_units;
+    probe.n_spheres = ds.n_spheres;
+    probe.n_boxes = ds.n_boxes;
+    if (lds_bytes(probe) > kMaxLds) {
+        set_error("rt_scene_update: scene needs more than 160 KiB of LDS");
+        return RT_ERR_UNSUPPORTED;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    // renders already queued on the context's stream may still read the blob
+    e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+    if (ds.blob_units > scene->capacity_units) {
+        void *nb = nullptr;
+        e = hipMalloc(&nb, blob.size() * sizeof(float4));
+        if (e != hipSuccess) return hip_fail("hipMalloc(scene)", e);
+        (void)hipFree(scene->dev.blob);
+        scene->dev.blob = nb;
+        scene->capacity_units = ds.blob_units;
+    }
+    e = hipMemcpy(scene->dev.blob, blob.data(), blob.size() * sizeof(float4), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail("hipMemcpy(scene)", e);
+    void *keep = scene->dev.blob;
+    scene->dev = ds;
+    scene->dev.blob = keep;
     return RT_OK;
 }
 

@@ -65,6 +65,7 @@ int main(int argc, char **argv) {
     rt_reference_materials(mats);
     rt_reference_lights(lights);
     std::vector<float> frame(static_cast<size_t>(width) * height * 4);
+    rt_scene *sc = nullptr;
     for (int k = 0; k < frames; ++k) {
         const float t = time0 + k * dt;
         std::vector<rt_object> objs;
@@ -81,10 +82,14 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "rt_cli: unknown scene %s\n", scene.c_str());
             return 2;
         }
-        rt_scene *sc = nullptr;
-        if (rt_scene_create(ctx, objs.data(), static_cast<int>(objs.size()), mats, RT_REFERENCE_MATERIALS, lights,
-                            RT_REFERENCE_LIGHTS, &sc) != RT_OK)
-            return fail("rt_scene_create");
+        if (!sc) {
+            if (rt_scene_create(ctx, objs.data(), static_cast<int>(objs.size()), mats, RT_REFERENCE_MATERIALS,
+                                lights, RT_REFERENCE_LIGHTS, &sc) != RT_OK)
+                return fail("rt_scene_create");
+        } else if (rt_scene_update(ctx, sc, objs.data(), static_cast<int>(objs.size()), mats, RT_REFERENCE_MATERIALS,
+                                   lights, RT_REFERENCE_LIGHTS) != RT_OK) {
+            return fail("rt_scene_update");
+        }
         const auto t0 = std::chrono::steady_clock::now();
         if (rt_render(ctx, sc, nullptr, t, width, height, depth, 0, height, frame.data(), 0, nullptr) != RT_OK)
             return fail("rt_render");
@@ -97,8 +102,8 @@ int main(int argc, char **argv) {
             return fail("rt_write_ppm");
         if (!pfm.empty() && rt_write_pfm(frame_name(pfm, k).c_str(), frame.data(), width, height) != RT_OK)
             return fail("rt_write_pfm");
-        rt_scene_destroy(sc);
     }
+    rt_scene_destroy(sc);
     rt_destroy(ctx);
     return 0;
 }

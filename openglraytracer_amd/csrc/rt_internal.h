@@ -135,4 +135,5 @@ struct rt_context {
 struct rt_scene {
     int device = 0;
     rtamd::DeviceScene dev;
+    int32_t capacity_units = 0;  // allocated blob size (16-B units)
 };

@@ -297,3 +297,19 @@ def test_monte_carlo_matches_oracle(gpu_ctx):
     f = rt.render(gpu_ctx, sc, w, h, 1, view=view)
     assert np.array_equal(acc.cpu().numpy(), (f + f) + f)
     sc.close()
+
+
+def test_scene_update_animation(gpu_ctx):
+    """rt_scene_update: the shipped scene animated over frames, one scene object."""
+    sc = rt.Scene(gpu_ctx, rt.reference_objects(0.0))
+    for t in [0.0, 1.5, 4.0]:
+        objs = rt.reference_objects(t)
+        sc.update(objs)
+        view = rt.make_view(None, t)
+        g = rt.render(gpu_ctx, sc, 64, 36, 1, view=view)
+        o = oracle_render(objs, 64, 36, 1, t)
+        assert np.array_equal(g, o)
+    sc.update(scenes.bench_objects(64))  # larger: reallocates
+    g = rt.render(gpu_ctx, sc, 64, 36, 1, view=rt.make_view(None, 0.0))
+    assert np.array_equal(g, oracle_render(scenes.bench_objects(64), 64, 36, 1))
+    sc.close()
