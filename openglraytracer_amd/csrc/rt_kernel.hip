@@ -109,6 +109,10 @@ __device__ __forceinline__ float glsl_exp2(float x) {
 }
 __device__ __forceinline__ float glsl_pow(float x, float y) { return glsl_exp2(glsl_log2(x) * y); }
 
+// Hardware sqrt (about 1 ulp, no correction steps): culling arithmetic only,
+// whose margins exceed its error by orders of magnitude.
+__device__ __forceinline__ float fsqrt_approx(float x) { return __builtin_amdgcn_sqrtf(x); }
+
 // ---- wave-wide reductions (called with all 64 lanes active) -------------
 // DPP butterfly within each 16-lane row, then row broadcasts; lane 63 holds
 // the result, read back as a wave-uniform value.
@@ -419,8 +423,8 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     // misses that cone by more than the margins cannot occlude any of them.
     const bool act = need && !hit;
     const v3 u = sub(p, L);
-    const float ul = __builtin_sqrtf(dot(u, u));
-    const v3 uh = ul > 0.0f ? muls(u, 1.0f / ul) : mk(0.0f, 0.0f, 0.0f);
+    const float ul = fsqrt_approx(dot(u, u));
+    const v3 uh = ul > 0.0f ? muls(u, __builtin_amdgcn_rcpf(ul)) : mk(0.0f, 0.0f, 0.0f);
     // cone axis: the direction of the first active lane
     const int lead = __builtin_ctzll(__ballot(act));
     const v3 ax = mk(lane_value(uh.x, lead), lane_value(uh.y, lead), lane_value(uh.z, lead));
@@ -450,7 +454,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         }
         return hit;
     }
-    const float sth = __builtin_sqrtf(fmaxf(0.0f, 1.0f - cmin * cmin));
+    const float sth = fsqrt_approx(fmaxf(0.0f, 1.0f - cmin * cmin));
     const int lane = threadIdx.x & 63;
     for (int base = 0; base < S.ns; base += 64) {
         const int k = base + lane;
@@ -459,7 +463,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
             const float4 c = S.sph[k];
             const float rad = __int_as_float(S.smeta[k].z);
             const v3 v = sub(mk(c.x, c.y, c.z), L);
-            const float d = __builtin_sqrtf(dot(v, v));
+            const float d = fsqrt_approx(dot(v, v));
             const float rp = rad + 0.021f + 1e-3f * d;  // 0.01 start offset + margins
             if (d <= rp) {
                 cand = true;
@@ -468,7 +472,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
             } else if (!angular) {
                 cand = true;
             } else {
-                const float sph = rp / d, cph = __builtin_sqrtf(fmaxf(0.0f, 1.0f - sph * sph));
+                const float sph = rp * __builtin_amdgcn_rcpf(d), cph = fsqrt_approx(fmaxf(0.0f, 1.0f - sph * sph));
                 const float cos_lim = cmin * cph - sth * sph;  // cos(theta + phi)
                 cand = !(dot(ax, v) < (cos_lim - 1e-3f) * d);
             }
@@ -738,7 +742,7 @@ __device__ int4 sphere_footprint(const LaunchParams &p, const FrameView &V, floa
         const float cx = P[0] * X + P[4] * Y + P[8] * Z + P[12];
         const float cy = P[1] * X + P[5] * Y + P[9] * Z + P[13];
         ok = ok && cw > 1e-4f;
-        const float iw = 1.0f / cw;
+        const float iw = __builtin_amdgcn_rcpf(cw);  // 2-pixel margin >> its error
         x0 = fminf(x0, cx * iw); x1 = fmaxf(x1, cx * iw);
         y0 = fminf(y0, cy * iw); y1 = fmaxf(y1, cy * iw);
     }

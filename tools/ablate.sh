@@ -1,11 +1,29 @@
 #!/bin/bash
-# Timing-only ablation builds of the kernel (outputs are wrong by design):
-# builds variants into build/ablate/<name>/ and times config 2 with each.
+# Timing-only builds of the kernel into tools/_ablate/<name>/:
+#   tools/ablate.sh            ablation variants (outputs wrong by design)
+#   tools/ablate.sh rev REV    the library as of git revision REV (A/B timing
+#                              against the working tree in one GPU call)
+#   tools/ablate.sh flags NAME "-DX ..."   the working tree with extra flags
 set -euo pipefail
 cd "$(dirname "$0")/.."
-for v in full:"" noshadow:"-DRT_ABLATE_SHADOW" nophong:"-DRT_ABLATE_PHONG" notrace:"-DRT_ABLATE_TRACE"; do
-  name=${v%%:*}; flag=${v#*:}
-  out=tools/_ablate/$name; mkdir -p $out/obj
-  make -s -C openglraytracer_amd/csrc OBJDIR=$(pwd)/$out/obj OUT=$(pwd)/$out/libopenglraytracer_amd.so CLI=/dev/null \
-       FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $flag" $(pwd)/$out/libopenglraytracer_amd.so
+build() {  # name srcdir extra-flags
+  local out=tools/_ablate/$1; mkdir -p $out/obj
+  make -s -C "$2" OBJDIR=$(pwd)/$out/obj OUT=$(pwd)/$out/libopenglraytracer_amd.so CLI=/dev/null \
+       FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $3" $(pwd)/$out/libopenglraytracer_amd.so
+}
+if [ "${1:-}" = rev ]; then
+  rev=${2:?revision}; src=tools/_ablate/rev_src
+  rm -rf $src tools/_ablate/rev; mkdir -p $src/pkg/csrc $src/include
+  for f in $(git ls-tree --name-only $rev openglraytracer_amd/csrc/); do git show $rev:$f > $src/pkg/csrc/$(basename $f); done
+  git show $rev:include/rt.h > $src/include/rt.h
+  build rev $src/pkg/csrc ""
+  exit 0
+fi
+if [ "${1:-}" = flags ]; then
+  build ${2:?name} openglraytracer_amd/csrc "${3:-}"
+  exit 0
+fi
+for v in full:"" noshadow:"-DRT_ABLATE_SHADOW" nophong:"-DRT_ABLATE_PHONG" notrace:"-DRT_ABLATE_TRACE" \
+         nostage:"-DRT_ABLATE_TRACE -DRT_ABLATE_STAGE" noraygen:"-DRT_ABLATE_TRACE -DRT_ABLATE_STAGE -DRT_ABLATE_RAYGEN"; do
+  build ${v%%:*} openglraytracer_amd/csrc "${v#*:}"
 done
