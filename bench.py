@@ -19,8 +19,9 @@ with one RCCL all-reduce: strong scaling; value = samples/s.
 
 value = primary rays (samples) of the step / step time (max over ranks), Mrays/s.
 roofline = the render kernel against the HBM-write roofline: 16 B per pixel
-(one float4 store) / average kernel time from HIP events around every launch
-of the timed region, on the launch stream.
+(one float4 store) / average kernel time from HIP events on the launch stream
+(N=1: one pair around the K back-to-back launches of the timed region; N>1:
+a pair around every launch).
 cpu_baseline = the reference's own shader on Mesa llvmpipe (oracle/_ref) over a
 bounded band of the same frame, in a child process on the host cores.
 
@@ -143,13 +144,17 @@ def main():
         px_per_launch = WIDTH * HEIGHT
         rays_per_step = MC_SPP * WIDTH * HEIGHT
 
-    # HIP events around every render launch of the timed region, on the
-    # stream the kernel is launched on
+    # Kernel time from HIP events on the stream the kernel is launched on. At
+    # N=1 a step is exactly one render launch: one event pair brackets the K
+    # back-to-back launches of the timed region (no markers between frames).
+    # At N>1 a pair brackets every render launch (the collective runs between).
+    ctx.set_timing(False)  # no per-launch markers of the library's own
+    per_launch = world > 1 or mc
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+          for _ in range(args.steps if per_launch else 1)]
 
     def step(timed, it=0):
-        if timed:
+        if timed and per_launch:
             ev[it][0].record(stream)
         if not mc:
             rt.render_batch(ctx, scene, buf.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS,
@@ -158,7 +163,7 @@ def main():
             accum.zero_()
             rt.render_accumulate(ctx, scene, accum.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, spp_mine, sample0,
                                  seed=0, view=view, stream=sh)
-        if timed:
+        if timed and per_launch:
             ev[it][1].record(stream)
         if not mc:
             if world > 1:
@@ -180,14 +185,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if not per_launch:
+        ev[0][0].record(stream)
     for it in range(args.steps):
         step(True, it)
+    if not per_launch:
+        ev[0][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    kernel_ms = [a.elapsed_time(b) for a, b in ev] if per_launch else [ev[0][0].elapsed_time(ev[0][1]) / args.steps]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -207,10 +207,15 @@ int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *
  * cannot be hit (conservative footprints / light cones with margins far
  * above float error) — output is bit-identical either way. */
 #define RT_OPT_CULLING 1
+/* RT_OPT_TIMING (default 1): record HIP events around every launch for
+ * rt_last_kernel_ms. Each event is a marker on the stream; 0 leaves the
+ * stream with the kernels alone (back-to-back launches, e.g. a benchmark
+ * timing many frames with one event pair of its own). */
+#define RT_OPT_TIMING 2
 int rt_context_set(rt_context *ctx, int option, int value);
 
-/* Kernel-only timing of the last rt_render/rt_render_shard on the context's
- * stream (ms, from HIP events around the launch). */
+/* Kernel-only timing of the last render call (ms, from HIP events around the
+ * launch on its stream); needs RT_OPT_TIMING. */
 int rt_last_kernel_ms(rt_context *ctx, float *ms);
 
 /* RGBA8 unorm packing of a float frame as the shipped GL_RGBA8 surface stores

@@ -190,6 +190,10 @@ class Context:
         """RT_OPT_CULLING: conservative sphere culling (output identical)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_CULLING, 1 if on else 0))
 
+    def set_timing(self, on):
+        """RT_OPT_TIMING: HIP events around every launch (for last_kernel_ms)."""
+        _check(lib().rt_context_set(self._h, abi.RT_OPT_TIMING, 1 if on else 0))
+
     def last_kernel_ms(self):
         ms = C.c_float()
         _check(lib().rt_last_kernel_ms(self._h, C.byref(ms)))

@@ -19,6 +19,7 @@ RT_MAX_OBJECTS = 1024
 RT_MAX_LIGHTS = 16
 RT_MAX_MATERIALS = 256
 RT_OPT_CULLING = 1
+RT_OPT_TIMING = 2
 RT_MAX_BATCH = 8
 
 # material indices of the reference table (raytrace_compute.glsl:74-157)

@@ -93,13 +93,16 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
 
 // Launch on `stream` with kernel-time events on the context.
 int launch(rt_context *ctx, const LaunchParams &p, int max_depth, hipStream_t stream) {
-    hipError_t e = hipEventRecord(ctx->ev0, stream);
-    if (e != hipSuccess) return hip_fail("hipEventRecord", e);
+    hipError_t e;
+    if (ctx->timing && (e = hipEventRecord(ctx->ev0, stream)) != hipSuccess) return hip_fail("hipEventRecord", e);
     e = launch_render(p, max_depth, stream);
     if (e != hipSuccess) return hip_fail("kernel launch", e);
-    e = hipEventRecord(ctx->ev1, stream);
-    if (e != hipSuccess) return hip_fail("hipEventRecord", e);
-    ctx->timed = true;
+    if (ctx->timing) {
+        if ((e = hipEventRecord(ctx->ev1, stream)) != hipSuccess) return hip_fail("hipEventRecord", e);
+        ctx->timed = true;
+    } else {
+        ctx->timed = false;
+    }
     return RT_OK;
 }
 
@@ -405,6 +408,7 @@ int rt_context_set(rt_context *ctx, int option, int value) {
     if (!ctx) { set_error("rt_context_set: null context"); return RT_ERR_INVALID; }
     switch (option) {
         case RT_OPT_CULLING: ctx->culling = value ? 1 : 0; return RT_OK;
+        case RT_OPT_TIMING: ctx->timing = value ? 1 : 0; return RT_OK;
         default: set_error("rt_context_set: unknown option " + std::to_string(option)); return RT_ERR_INVALID;
     }
 }

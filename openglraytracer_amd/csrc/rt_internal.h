@@ -130,6 +130,7 @@ struct rt_context {
     size_t staging_px = 0;
     bool timed = false;
     int culling = 1;  // RT_OPT_CULLING
+    int timing = 1;   // RT_OPT_TIMING
 };
 
 struct rt_scene {

@@ -41,8 +41,16 @@
 namespace rtamd {
 namespace {
 
-constexpr int kTile = 16;  // pixels per tile edge
-constexpr int kThreads = 256;
+#ifndef RT_WAVES_X
+#define RT_WAVES_X 2
+#endif
+#ifndef RT_WAVES_Y
+#define RT_WAVES_Y 2
+#endif
+// A work-group renders a tile of kWavesX x kWavesY wave footprints of 8x8 pixels.
+constexpr int kWavesX = RT_WAVES_X, kWavesY = RT_WAVES_Y;
+constexpr int kTileX = 8 * kWavesX, kTileY = 8 * kWavesY;
+constexpr int kThreads = 64 * kWavesX * kWavesY;
 
 struct v3 {
     float x, y, z;
@@ -164,7 +172,8 @@ struct Hit {
     float t;
     int obj;      // reference index, -1 = none
     int slot;     // sphere slot (>= 0) or ~box slot (< 0)
-    bool inside;  // sphere: t_near < 0 (:621)
+    bool inside;  // t_near < 0: the ray leaves the object (:621, :693-696)
+    v3 bnd;       // box: the slab distances t is the minimum / maximum of (:690-696)
 };
 
 __device__ __forceinline__ bool closer(float t, int obj, const Hit &h) {
@@ -222,14 +231,20 @@ __device__ __forceinline__ v3 exits(const BoxRec &b, v3 rs, v3 rd) {
     return mk(exit_num(b.mins[0], b.maxs[0], rs.x, rd.x) / rd.x, exit_num(b.mins[1], b.maxs[1], rs.y, rd.y) / rd.y,
               exit_num(b.mins[2], b.maxs[2], rs.z, rd.z) / rd.z);
 }
-// Box t for the closest-hit loop. With the origin strictly inside and no NaN
-// in the direction: t_near < 0 < t_far, so t = t_far (:690-696).
-__device__ __forceinline__ float box_t(const BoxRec &b, v3 rs, v3 rd, bool inside) {
+// Box t for the closest-hit loop (-1 on a miss), with the slab distances the
+// collision record's face test needs (bnd: t1 when entering, t2 when leaving)
+// and whether the ray leaves the box. With the origin strictly inside and no
+// NaN in the direction: t_near < 0 < t_far, so t = t_far (:690-696).
+__device__ __forceinline__ float box_t(const BoxRec &b, v3 rs, v3 rd, bool inside, v3 &bnd, bool &leaving) {
     if (inside && not_nan(rd)) {
-        const v3 e = exits(b, rs, rd);
-        return gmin(gmin(e.x, e.y), e.z);
+        bnd = exits(b, rs, rd);
+        leaving = true;
+        return gmin(gmin(bnd.x, bnd.y), bnd.z);
     }
-    return slab_t(slab(b, rs, rd));
+    const Slab sl = slab(b, rs, rd);
+    leaving = sl.t_near < 0.0f;
+    bnd = sel(leaving, sl.t2, sl.t1);
+    return slab_t(sl);
 }
 // fl(num / d) < 1 for a non-negative quotient, dividing only when |num| is
 // within 2^-16 of |d| (correctly rounded division is monotonic).
@@ -291,7 +306,12 @@ __device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 
         bool inside = false;
         const float t = sphere_t(qb, qc, qa2, qa4, inside);
         const int obj = S.smeta[s].x;
-        if (closer(t, obj, h)) h = {t, obj, s, inside};
+        if (closer(t, obj, h)) {
+            h.t = t;
+            h.obj = obj;
+            h.slot = s;
+            h.inside = inside;
+        }
     }
 }
 
@@ -322,7 +342,7 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
 __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
-    Hit h{10000.0f, -1, 0, false};
+    Hit h{10000.0f, -1, 0, false, mk(0.0f, 0.0f, 0.0f)};
     for (int b = 0; b < S.nb; ++b) {
         const BoxRec &B = S.box[b];
         v3 rs;
@@ -335,8 +355,10 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
             rs = xform_point(B.w2l, r.start);
             inside = strictly_inside(B, rs);
         }
-        const float t = box_t(B, rs, xform_dir(B.w2l, r.dir), inside);
-        if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, false};
+        v3 bnd;
+        bool leaving;
+        const float t = box_t(B, rs, xform_dir(B.w2l, r.dir), inside, bnd, leaving);
+        if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, leaving, bnd};
     }
     const v3 d2 = muls(r.dir, 2.0f);
     const float qa = dot(r.dir, r.dir);
@@ -495,6 +517,9 @@ struct Collision {
 };
 
 // Build the collision record of the winning object (:628-637, :686-721).
+// A box's slab distances come with the hit (the closest-hit loop computed
+// them); its t is the slab test's intersection distance.
+template <bool kPrimary>
 __device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const Hit &h, bool valid) {
     Collision c;
     c.p = mk(0.0f, 0.0f, 0.0f);
@@ -513,23 +538,17 @@ __device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const
     } else {
         const BoxRec &B = S.box[~h.slot];
         c.material = B.material;
-        const v3 rs = xform_point(B.w2l, r.start), rd = xform_dir(B.w2l, r.dir);
-        float isect;
-        v3 boundary;
-        if (strictly_inside(B, rs) && not_nan(rd)) {  // t_near < 0: leaving the box
-            boundary = exits(B, rs, rd);
-            isect = gmin(gmin(boundary.x, boundary.y), boundary.z);
-            c.inside = true;
+        v3 rs;
+        if (kPrimary) {
+            const float4 bc = S.box_cam[~h.slot];
+            rs = mk(bc.x, bc.y, bc.z);
         } else {
-            const Slab s = slab(B, rs, rd);
-            isect = s.t_near;
-            boundary = s.t1;
-            if (s.t_near < 0.0f) {
-                isect = s.t_far;
-                boundary = s.t2;
-                c.inside = true;
-            }
+            rs = xform_point(B.w2l, r.start);
         }
+        const v3 rd = xform_dir(B.w2l, r.dir);
+        const float isect = h.t;
+        const v3 boundary = h.bnd;
+        c.inside = h.inside;
         int face = 0;
         if (isect == boundary.y) face = 1;
         else if (isect == boundary.z) face = 2;
@@ -611,7 +630,7 @@ __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     const Hit h = closest<true>(S, r, valid);
     const bool hit = valid && h.obj >= 0;
     if (!__any(hit)) return black;  // per-wave early out
-    const Collision c = resolve(S, r, h, hit);
+    const Collision c = resolve<true>(S, r, h, hit);
 #ifdef RT_ABLATE_PHONG
     const v3 col = add(c.p, c.n);
 #else
@@ -628,7 +647,8 @@ struct Frame {
 };
 
 template <int N>
-struct Frames {  // register-resident: every access uses a compile-time index
+struct Frames {  // per-level frames; dynamically indexed (the compiler keeps them in scratch,
+                 // measured faster than per-field register selects at depth 2)
     Frame f[N];
     __device__ __forceinline__ Frame get(int level) const {
         Frame r = f[0];
@@ -654,10 +674,11 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
     bool first = true;
     while (__any(!done)) {
         const bool valid = !done;
+        const bool primary = first;
         const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
         first = false;
         const bool hit = valid && h.obj >= 0;
-        const Collision c = resolve(S, ray, h, hit);
+        const Collision c = primary ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
 #ifdef RT_ABLATE_PHONG
         const v3 col = add(c.p, c.n);
 #else
@@ -773,8 +794,13 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
     return static_cast<float>(h >> 8) * (1.0f / 16777216.0f);
 }
 
+#ifdef RT_WAVES_PER_EU
+#define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, RT_WAVES_PER_EU)))
+#else
+#define RT_OCCUPANCY
+#endif
 template <int kDepth, bool kAccum>
-__global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
+__global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     // ---- stage the scene blob into LDS (one pass per work-group) ----
     const float4 *blob = static_cast<const float4 *>(p.scene);
@@ -788,6 +814,9 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
     {
         const float4 *sph = lds + p.off_spheres;
         const int4 *smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
+#ifdef RT_ABLATE_SETUP
+        if (p.n_spheres < 0)
+#endif
         for (int s = threadIdx.x; s < p.n_spheres; s += kThreads) {
             const float4 c = sph[s];
             const v3 oc = sub(origin, mk(c.x, c.y, c.z));
@@ -821,13 +850,13 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
 
     // ---- this lane's pixel: wave w covers the 8x8 quadrant w of the tile ----
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * kTile + (wave & 1) * 8 + (lane & 7);
-    const int lr0 = blockIdx.y * kTile + (wave >> 1) * 8;
+    const int x = blockIdx.x * kTileX + (wave % kWavesX) * 8 + (lane & 7);
+    const int lr0 = blockIdx.y * kTileY + (wave / kWavesX) * 8;
     const int local_row = lr0 + (lane >> 3);
     const bool active = x < p.width && local_row < p.n_rows;
     if (!__any(active)) return;
     const int y = output_row(p, active ? local_row : lr0);
-    S.tx0 = blockIdx.x * kTile + (wave & 1) * 8;
+    S.tx0 = blockIdx.x * kTileX + (wave % kWavesX) * 8;
     S.tx1 = S.tx0 + 7;
     S.ty0 = INT_MAX;
     S.ty1 = INT_MIN;
@@ -863,7 +892,9 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
 
     if constexpr (!kAccum) {
         const Ray ray = camera_ray(0.0f, 0.0f);
-#ifdef RT_ABLATE_TRACE
+#if defined(RT_ABLATE_RAYGEN)
+        const v3 col = mk(float(x), float(y), 0.0f);
+#elif defined(RT_ABLATE_TRACE)
         const v3 col = ray.dir;
 #else
         v3 col;
@@ -892,7 +923,7 @@ __global__ __launch_bounds__(kThreads) void render_kernel(LaunchParams p) {
 
 template <int kDepth>
 hipError_t launch_depth(const LaunchParams &p, hipStream_t stream) {
-    const dim3 grid((p.width + kTile - 1) / kTile, (p.n_rows + kTile - 1) / kTile, p.n_views);
+    const dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY - 1) / kTileY, p.n_views);
     if (p.spp > 0)
         hipLaunchKernelGGL((render_kernel<kDepth, true>), grid, dim3(kThreads), lds_bytes(p), stream, p);
     else

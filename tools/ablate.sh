@@ -9,7 +9,7 @@ cd "$(dirname "$0")/.."
 build() {  # name srcdir extra-flags
   local out=tools/_ablate/$1; mkdir -p $out/obj
   make -s -C "$2" OBJDIR=$(pwd)/$out/obj OUT=$(pwd)/$out/libopenglraytracer_amd.so CLI=/dev/null \
-       FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off $3" $(pwd)/$out/libopenglraytracer_amd.so
+       FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize $3" $(pwd)/$out/libopenglraytracer_amd.so
 }
 if [ "${1:-}" = rev ]; then
   rev=${2:?revision}; src=tools/_ablate/rev_src
