@@ -119,8 +119,15 @@ def main():
 
     ctx = rt.Context(device)
     scene = rt.Scene(ctx, rt.bench_objects(N_SPHERES, 0))
-    stream = torch.cuda.current_stream()
+    # a stream of our own, made current: the render launches, the events and
+    # the collectives are ordered on it and the launches are asynchronous (the
+    # C-ABI treats a NULL stream — torch's default stream handle is 0 — as
+    # "synchronous on the context's stream", like glFinish)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
+    assert sh, "need a non-default HIP stream"
+
     mc = args.workload == "config5"
 
     if not mc:

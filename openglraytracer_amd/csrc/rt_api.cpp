@@ -86,13 +86,16 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.off_lights = d.off_lights;
     p.off_lightmat = d.off_lightmat;
     p.off_bvh = d.off_bvh;
+    p.off_cone = d.off_cone;
     p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
     return p;
 }
 
 // Launch on `stream` with kernel-time events on the context.
-int launch(rt_context *ctx, const LaunchParams &p, int max_depth, hipStream_t stream) {
+int launch(rt_context *ctx, LaunchParams &p, int max_depth, hipStream_t stream) {
+    p.n_cu = ctx->n_cu;
+    p.sched = ctx->sched + static_cast<size_t>(ctx->sched_next++ % kSchedSlots) * kSchedInts;
     hipError_t e;
     if (ctx->timing && (e = hipEventRecord(ctx->ev0, stream)) != hipSuccess) return hip_fail("hipEventRecord", e);
     e = launch_render(p, max_depth, stream);
@@ -132,6 +135,9 @@ int rt_create(int device, rt_context **out) {
     ctx->device = device;
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess ||
+        (e = hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess ||
+        (e = hipMalloc(&ctx->sched, sizeof(int32_t) * kSchedInts * kSchedSlots)) != hipSuccess ||
+        (e = hipMemset(ctx->sched, 0, sizeof(int32_t) * kSchedInts * kSchedSlots)) != hipSuccess ||
         (e = allow_large_lds(kMaxLds)) != hipSuccess) {
         rt_destroy(ctx);
         return hip_fail("rt_create", e);
@@ -145,6 +151,7 @@ void rt_destroy(rt_context *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->staging) (void)hipFree(ctx->staging);
+    if (ctx->sched) (void)hipFree(ctx->sched);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -53,10 +53,28 @@ struct MatRec {
     float emissive[4];
     float shininess, reflectivity, transparency, refraction_index;
 };  // 48 B
+// The flags decide whether a light's direct term can change the Phong sums;
+// the shadow ray is cast only then (lit and shadowed agree otherwise):
+// d_nz / s_nz: some component of Ld*Md / Ls*Ms is nonzero; always: the
+// material is not "tame" (a product is not finite, or the shininess is not a
+// positive finite number), so the diffuse / specular factors may be NaN or
+// infinite and every light's term is taken as changing the sums.
 struct LightMatRec {
     float ld_md[4];
     float ls_ms[4];
+    int32_t d_nz, s_nz, always, pad;
+};  // 48 B
+// Shadow-ray culling cone of sphere s seen from light j (host, float64):
+// v = unit direction light -> centre; far = d - rp where d = |centre - light|
+// and rp = |radius| + 0.021 + 1e-3 d (the 0.01 start offset plus margins);
+// sin / cos of the half-angle asin(rp / d); near = 1 when d <= rp (the light
+// is inside the inflated sphere: always a candidate).
+struct ShadowCone {
+    float v[3];
+    float far;
+    float sph, cph, near, pad;
 };  // 32 B
+constexpr size_t kConeLdsBudget = 24 * 1024;
 // Sphere BVH node (depth-first order; the left child is the next node):
 // lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
 // this subtree (-1: end) and leaf = (count << 24) | first sphere slot (0 for
@@ -97,19 +115,31 @@ struct LaunchParams {
     float4 *out;        // n_views x n_rows x width float4
     int32_t off_spheres, off_smeta, off_boxes, off_mats, off_lights, off_lightmat;  // 16-B units
     int32_t off_bvh, n_bvh;  // sphere BVH nodes (2 x float4 each), 16-B units / count
+    int32_t off_cone;        // n_lights x n_spheres ShadowCone, 16-B units; -1: none
+                             // (kept only while the LDS total stays within kConeLdsBudget)
     int32_t blob_units;      // blob size, 16-B units
     // Monte-Carlo accumulation (render_kernel<D, true>): samples
     // [sample0, sample0 + spp) per pixel, jittered inside the pixel when
     // jitter != 0, summed in sample order and added to out.
     int32_t spp, sample0, jitter;
     uint32_t seed;
+    // Queued work distribution (rt_kernel.hip, render_kernel): the counters of
+    // this launch (kSchedInts zeroed ints, left zeroed by the kernel), and the
+    // compute units the resident grid is sized for. nullptr: one work-group
+    // per tile.
+    int32_t *sched;
+    int32_t n_cu;
 };
+constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
+constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
+constexpr int kSchedInts = 2 * kQueues * kQueueStride; // heads + done counters of one launch
+constexpr int kSchedSlots = 64;                        // launches that may be in flight at once
 
 struct DeviceScene {
     void *blob = nullptr;
     int32_t blob_units = 0;
     int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
-    int32_t off_bvh = 0, n_bvh = 0;
+    int32_t off_bvh = 0, n_bvh = 0, off_cone = 0;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
 
@@ -131,6 +161,9 @@ struct rt_context {
     bool timed = false;
     int culling = 1;  // RT_OPT_CULLING
     int timing = 1;   // RT_OPT_TIMING
+    int n_cu = 0;               // compute units of the device
+    int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
+    unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots
 };
 
 struct rt_scene {

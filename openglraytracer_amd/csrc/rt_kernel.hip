@@ -33,6 +33,7 @@
 // lanes; divergence is confined to the innermost exact tests.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 
@@ -62,8 +63,47 @@ __device__ __forceinline__ v3 muls(v3 a, float s) { return {a.x * s, a.y * s, a.
 __device__ __forceinline__ v3 sel(bool c, v3 a, v3 b) { return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z}; }
 // dot(vec3) as llvmpipe associates it: x + (y + z)
 __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
-// normalize(v) = v * inversesqrt(dot(v, v)), inversesqrt = 1 / sqrt (IEEE)
-__device__ __forceinline__ v3 normalize(v3 a) { return muls(a, 1.0f / sqrtf(dot(a, a))); }
+
+// ---- correctly rounded division and square root, short forms -------------
+// hipcc lowers a / b (IEEE) to div_scale(b), rcp, 2 fma (the refined
+// reciprocal r), div_scale(a), mul, 3 fma, div_fmas, div_fixup; and sqrtf(x)
+// to a scale-up of tiny x, v_sqrt, two one-ulp probes with fma, the
+// scale-down and a class fix-up. For operands of moderate magnitude the scale
+// steps are identities and the fix-ups return their input, so the arithmetic
+// that remains — written out below in the same order — is the same correctly
+// rounded result in fewer instructions, and a reciprocal shared by several
+// quotients is refined once. Valid ranges: div_r needs b normal with
+// |b| in [2^-60, 2^60] and a = +0 or |a| in [2^-60, 2^60]; sqrt_short needs
+// x >= 2^-96 (or +inf). Callers prove the range or check it per wave.
+struct Rcp {
+    float b, r;
+};
+__device__ __forceinline__ Rcp rcp_refined(float b) {
+    float r = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    return {b, r};
+}
+__device__ __forceinline__ float div_r(float a, Rcp d) {
+    float q = a * d.r;
+    float t = __builtin_fmaf(-d.b, q, a);
+    q = __builtin_fmaf(t, d.r, q);
+    t = __builtin_fmaf(-d.b, q, a);
+    return __builtin_fmaf(t, d.r, q);
+}
+__device__ __forceinline__ float sqrt_short(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float dn = __uint_as_float(__float_as_uint(s) - 1u), up = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r = __builtin_fmaf(-dn, s, x) <= 0.0f ? dn : s;
+    return __builtin_fmaf(-up, s, x) > 0.0f ? up : r;
+}
+// 1 / sqrt(d), both correctly rounded (GLSL inversesqrt as llvmpipe evaluates it)
+__device__ __forceinline__ float inv_sqrt(float d) {
+    if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return div_r(1.0f, rcp_refined(sqrt_short(d)));
+    return 1.0f / sqrtf(d);
+}
+// normalize(v) = v * inversesqrt(dot(v, v))
+__device__ __forceinline__ v3 normalize(v3 a) { return muls(a, inv_sqrt(dot(a, a))); }
 __device__ __forceinline__ float gmin(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float gmax(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float comp(v3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
@@ -104,7 +144,8 @@ __device__ __forceinline__ float glsl_log2(float x) {
     const uint32_t i = __float_as_uint(x);
     const float e = static_cast<float>(static_cast<int>((i >> 23) & 0xffu) - 127);
     const float mant = __uint_as_float((i & 0x007fffffu) | 0x3f800000u);
-    const float y = (mant - 1.0f) / (mant + 1.0f);
+    // mant - 1 is +0 or at least 2^-23, mant + 1 in [2, 3): the short division is exact
+    const float y = div_r(mant - 1.0f, rcp_refined(mant + 1.0f));
     return __builtin_fmaf(y, poly_log2(y * y), e);
 }
 __device__ __forceinline__ float glsl_exp2(float x) {
@@ -162,6 +203,7 @@ struct Scene {
     const LightRec *light;
     const LightMatRec *lm;
     const float4 *bvh;  // BvhNode pairs (lo, hi)
+    const ShadowCone *cone;  // [light][sphere] shadow culling cones
     int ns, nb, nl, nm, nbvh;
     int cull;
     int tx0, tx1, ty0, ty1;  // this wave's pixel rectangle (frame coordinates)
@@ -478,25 +520,45 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     }
     const float sth = fsqrt_approx(fmaxf(0.0f, 1.0f - cmin * cmin));
     const int lane = threadIdx.x & 63;
+    const ShadowCone *cones = S.cone ? S.cone + light * S.ns : nullptr;
     for (int base = 0; base < S.ns; base += 64) {
         const int k = base + lane;
         bool cand = false;
         if (k < S.ns) {
-            const float4 c = S.sph[k];
-            const float rad = __int_as_float(S.smeta[k].z);
-            const v3 v = sub(mk(c.x, c.y, c.z), L);
-            const float d = fsqrt_approx(dot(v, v));
-            const float rp = rad + 0.021f + 1e-3f * d;  // 0.01 start offset + margins
-            if (d <= rp) {
-                cand = true;
-            } else if (d - rp > maxlen) {
+            // the sphere's cone from the light: precomputed (host, float64) or
+            // derived here with approximate sqrt / rcp (same margins)
+            float far, sph, cph;
+            v3 v;
+            bool near;
+            if (cones) {
+                const ShadowCone &sc = cones[k];
+                v = mk(sc.v[0], sc.v[1], sc.v[2]);
+                far = sc.far;
+                sph = sc.sph;
+                cph = sc.cph;
+                near = sc.near != 0.0f;
+            } else {
+                const float4 c = S.sph[k];
+                const float rad = __int_as_float(S.smeta[k].z);
+                v = sub(mk(c.x, c.y, c.z), L);
+                const float d = fsqrt_approx(dot(v, v));
+                const float rp = rad + 0.021f + 1e-3f * d;  // 0.01 start offset + margins
+                near = d <= rp;
+                far = d - rp;
+                const float id = __builtin_amdgcn_rcpf(d);
+                v = muls(v, id);
+                sph = rp * id;
+                cph = fsqrt_approx(fmaxf(0.0f, 1.0f - sph * sph));
+            }
+            if (near) {
+                cand = true;  // light inside the inflated sphere
+            } else if (far > maxlen) {
                 cand = false;  // beyond every shaded point
             } else if (!angular) {
                 cand = true;
             } else {
-                const float sph = rp * __builtin_amdgcn_rcpf(d), cph = fsqrt_approx(fmaxf(0.0f, 1.0f - sph * sph));
                 const float cos_lim = cmin * cph - sth * sph;  // cos(theta + phi)
-                cand = !(dot(ax, v) < (cos_lim - 1e-3f) * d);
+                cand = !(dot(ax, v) < cos_lim - 1e-3f);
             }
         }
         uint64_t mask = __ballot(cand);
@@ -587,11 +649,10 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
                                       dif.w + q.ld_md[3] * kd);
         const float4 ns = make_float4(spe.x + q.ls_ms[0] * ks, spe.y + q.ls_ms[1] * ks, spe.z + q.ls_ms[2] * ks,
                                       spe.w + q.ls_ms[3] * ks);
-        const bool changes =
-            __float_as_uint(nd.x) != __float_as_uint(dif.x) || __float_as_uint(nd.y) != __float_as_uint(dif.y) ||
-            __float_as_uint(nd.z) != __float_as_uint(dif.z) || __float_as_uint(nd.w) != __float_as_uint(dif.w) ||
-            __float_as_uint(ns.x) != __float_as_uint(spe.x) || __float_as_uint(ns.y) != __float_as_uint(spe.y) ||
-            __float_as_uint(ns.z) != __float_as_uint(spe.z) || __float_as_uint(ns.w) != __float_as_uint(spe.w);
+        // the shadow ray matters only if the light's term can change the sums
+        // (host flags, rt_scene.cpp: with a tame material a zero factor or a
+        // zero product adds +-0 to sums that are never -0)
+        const bool changes = q.always || (kd != 0.0f && q.d_nz) || (ks != 0.0f && q.s_nz);
         const bool need = valid && changes;
 #ifdef RT_ABLATE_SHADOW
         if (need) { dif = nd; spe = ns; }
@@ -794,69 +855,52 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
     return static_cast<float>(h >> 8) * (1.0f / 16777216.0f);
 }
 
-#ifdef RT_WAVES_PER_EU
-#define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU, RT_WAVES_PER_EU)))
-#else
-#define RT_OCCUPANCY
+// Occupancy target per depth: the recursive kernels (depth >= 2) keep the
+// tree walk's frames in scratch either way and hide its latency best at 6
+// waves per SIMD (config 4: 58 -> 37 ms; config 3: 1.52 -> 1.37 ms); depth 0/1
+// need fewer registers than that anyway.
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU(d) ((d) >= 2 ? 6 : 1)
 #endif
-template <int kDepth, bool kAccum>
-__global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    // ---- stage the scene blob into LDS (one pass per work-group) ----
-    const float4 *blob = static_cast<const float4 *>(p.scene);
-    for (int i = threadIdx.x; i < p.blob_units; i += kThreads) lds[i] = blob[i];
-    float4 *sph_cam = lds + p.blob_units;
-    int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
-    float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
-    __syncthreads();
-    const FrameView &V = p.view[blockIdx.z];
+#define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(kDepth))))
+// Per-frame constants of one view into LDS: the camera-origin terms of every
+// sphere (oc, qc :587-588) and box (local origin :655, strictly-inside flag)
+// and every sphere's conservative pixel footprint.
+__device__ __forceinline__ void frame_setup(const LaunchParams &p, const FrameView &V, const float4 *lds,
+                                            float4 *sph_cam, int4 *sph_px, float4 *box_cam) {
     const v3 origin = mk(V.origin[0], V.origin[1], V.origin[2]);
-    {
-        const float4 *sph = lds + p.off_spheres;
-        const int4 *smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
+    const float4 *sph = lds + p.off_spheres;
+    const int4 *smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
 #ifdef RT_ABLATE_SETUP
-        if (p.n_spheres < 0)
+    if (p.n_spheres < 0)
 #endif
-        for (int s = threadIdx.x; s < p.n_spheres; s += kThreads) {
-            const float4 c = sph[s];
-            const v3 oc = sub(origin, mk(c.x, c.y, c.z));
-            sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);
-            sph_px[s] = sphere_footprint(p, V, c, __int_as_float(smeta[s].z));
-        }
-        const BoxRec *box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
-        for (int b = threadIdx.x; b < p.n_boxes; b += kThreads) {
-            const v3 rs = xform_point(box[b].w2l, origin);
-            box_cam[b] = make_float4(rs.x, rs.y, rs.z, strictly_inside(box[b], rs) ? 1.0f : 0.0f);
-        }
+    for (int s = threadIdx.x; s < p.n_spheres; s += kThreads) {
+        const float4 c = sph[s];
+        const v3 oc = sub(origin, mk(c.x, c.y, c.z));
+        sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);
+        sph_px[s] = sphere_footprint(p, V, c, __int_as_float(smeta[s].z));
     }
-    __syncthreads();
-    Scene S;
-    S.sph = lds + p.off_spheres;
-    S.smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
-    S.sph_cam = sph_cam;
-    S.sph_px = sph_px;
-    S.box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
-    S.box_cam = box_cam;
-    S.mat = reinterpret_cast<const MatRec *>(lds + p.off_mats);
-    S.light = reinterpret_cast<const LightRec *>(lds + p.off_lights);
-    S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
-    S.bvh = lds + p.off_bvh;
-    S.nbvh = p.n_bvh;
-    S.ns = p.n_spheres;
-    S.nb = p.n_boxes;
-    S.nl = p.n_lights;
-    S.nm = p.n_mats;
-    S.cull = V.cull;
+    const BoxRec *box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
+    for (int b = threadIdx.x; b < p.n_boxes; b += kThreads) {
+        const v3 rs = xform_point(box[b].w2l, origin);
+        box_cam[b] = make_float4(rs.x, rs.y, rs.z, strictly_inside(box[b], rs) ? 1.0f : 0.0f);
+    }
+}
 
-    // ---- this lane's pixel: wave w covers the 8x8 quadrant w of the tile ----
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * kTileX + (wave % kWavesX) * 8 + (lane & 7);
-    const int lr0 = blockIdx.y * kTileY + (wave / kWavesX) * 8;
+// One 8x8 wave tile (wx, wy) of view z: lane l renders pixel (8 wx + l % 8, 8 wy + l / 8).
+template <int kDepth, bool kAccum>
+__device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
+                                                 int z) {
+    const v3 origin = mk(V.origin[0], V.origin[1], V.origin[2]);
+    S.cull = V.cull;
+    const int lane = threadIdx.x & 63;
+    const int x = wx * 8 + (lane & 7);
+    const int lr0 = wy * 8;
     const int local_row = lr0 + (lane >> 3);
     const bool active = x < p.width && local_row < p.n_rows;
     if (!__any(active)) return;
     const int y = output_row(p, active ? local_row : lr0);
-    S.tx0 = blockIdx.x * kTileX + (wave % kWavesX) * 8;
+    S.tx0 = wx * 8;
     S.tx1 = S.tx0 + 7;
     S.ty0 = INT_MAX;
     S.ty1 = INT_MIN;
@@ -871,9 +915,21 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     const float *M = V.unproj;  // column-major
     // jx, jy: sub-pixel offsets of a Monte-Carlo sample (0 for the
     // reference's one ray per pixel; float(x - hw) + 0.0f is exact)
+    // x - hw + jx is +0 or a multiple of 2^-24 of magnitude <= 2^16: the
+    // short division by the (uniform) W/2, H/2 >= 1 is the correctly rounded
+    // one (a 1-pixel-wide or -high frame divides by 0: IEEE path)
+    const Rcp rw = rcp_refined(static_cast<float>(hw)), rh = rcp_refined(static_cast<float>(hh));
+    const bool halves_ok = hw > 0 && hh > 0;
     auto camera_ray = [&](float jx, float jy) {
-        const float vx = (static_cast<float>(x - hw) + jx) / static_cast<float>(hw);
-        const float vy = (static_cast<float>(y - hh) + jy) / static_cast<float>(hh);
+        const float nx = static_cast<float>(x - hw) + jx, ny = static_cast<float>(y - hh) + jy;
+        float vx, vy;
+        if (halves_ok) {
+            vx = div_r(nx, rw);
+            vy = div_r(ny, rh);
+        } else {
+            vx = nx / static_cast<float>(hw);
+            vy = ny / static_cast<float>(hh);
+        }
         float ws[4], we[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -887,7 +943,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
         ray.dir = normalize(sub(e3, s3));
         return ray;
     };
-    float4 *out = p.out + static_cast<size_t>(blockIdx.z) * p.n_rows * p.width;
+    float4 *out = p.out + static_cast<size_t>(z) * p.n_rows * p.width;
     const size_t idx = static_cast<size_t>(local_row) * p.width + x;
 
     if constexpr (!kAccum) {
@@ -921,14 +977,131 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     }
 }
 
+// Work distribution.
+//  * Tiled (p.sched == nullptr, or a launch of several views): one work-group
+//    per kTileX x kTileY tile of a view (blockIdx.z), wave w rendering its
+//    8x8 quadrant; the scene and the view's per-frame constants are staged
+//    into LDS per work-group.
+//  * Queued (depth >= 2, one view, more wave tiles than resident waves,
+//    p.sched set): a grid of as many work-groups as are
+//    resident at once; each stages the scene and the per-frame constants
+//    once, then every wave renders 8x8 wave tiles on its own until the frame
+//    is done — no barrier after the prologue, and the frame ends on
+//    wave-tile granularity instead of with a tail of late work-groups. The
+//    wave tiles are dealt to kQueues queues by index (tile t in queue
+//    t % kQueues, spatially interleaved, so the queues carry equal work);
+//    global wave g belongs to queue g % kQueues, starts with tile g and then
+//    takes the queue's next tile from its atomic head, fetched one tile
+//    ahead. The last wave of a queue to run dry resets the queue's head and
+//    done counters for the next launch.
+// Queued distribution pays where the cost per wave tile varies most (the
+// recursive depths); depth 0 / 1 keep the tiled kernel, whose body the
+// compiler schedules with fewer registers (config 2: 70 vs 81 VGPRs).
+constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
+
+template <int kDepth, bool kAccum>
+__global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    // ---- stage the scene blob into LDS (one pass per work-group) ----
+    const float4 *blob = static_cast<const float4 *>(p.scene);
+    for (int i = threadIdx.x; i < p.blob_units; i += kThreads) lds[i] = blob[i];
+    float4 *sph_cam = lds + p.blob_units;
+    int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
+    float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
+    __syncthreads();
+    const bool queued = kQueuedDepth(kDepth) && p.sched != nullptr;
+    const int z = queued ? 0 : static_cast<int>(blockIdx.z);
+    const FrameView &V = p.view[z];
+    frame_setup(p, V, lds, sph_cam, sph_px, box_cam);
+    __syncthreads();
+    Scene S;
+    S.sph = lds + p.off_spheres;
+    S.smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
+    S.sph_cam = sph_cam;
+    S.sph_px = sph_px;
+    S.box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
+    S.box_cam = box_cam;
+    S.mat = reinterpret_cast<const MatRec *>(lds + p.off_mats);
+    S.light = reinterpret_cast<const LightRec *>(lds + p.off_lights);
+    S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
+    S.bvh = lds + p.off_bvh;
+    S.cone = p.off_cone >= 0 ? reinterpret_cast<const ShadowCone *>(lds + p.off_cone) : nullptr;
+    S.nbvh = p.n_bvh;
+    S.ns = p.n_spheres;
+    S.nb = p.n_boxes;
+    S.nl = p.n_lights;
+    S.nm = p.n_mats;
+    // wave index through readfirstlane: provably wave-uniform to the compiler,
+    // so the tile coordinates and culling rectangles stay in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int wtx = (p.width + 7) / 8;
+    const int total = queued ? wtx * ((p.n_rows + 7) / 8) : 1;
+    const int g = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave;  // global wave
+    const int n_waves = static_cast<int>(gridDim.x) * (kThreads / 64);
+    const int q = g % kQueues;
+    const int q_waves = (n_waves - q + kQueues - 1) / kQueues;  // waves of queue q
+    int *head = p.sched + q * kQueueStride;
+    int *done = p.sched + (kQueues + q) * kQueueStride;
+    // tiled: the wave's quadrant of the block's tile; queued: item g / kQueues
+    // of queue q (its first q_waves items are dealt statically), then the
+    // queue's head (one render call site for both: the kernel body is inlined once)
+    int t = queued ? g : 0;
+    while (t < total) {
+        int nxt = 0;
+        if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
+        const int wx = queued ? t % wtx : static_cast<int>(blockIdx.x) * kWavesX + wave % kWavesX;
+        const int wy = queued ? t / wtx : static_cast<int>(blockIdx.y) * kWavesY + wave / kWavesX;
+        render_wave_tile<kDepth, kAccum>(p, S, V, wx, wy, z);
+        t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
+    }
+    if (!queued) return;
+    if (lane == 0 && atomicAdd(done, 1) == q_waves - 1) {
+        atomicExch(head, 0);  // every wave of the queue has made its last fetch
+        atomicExch(done, 0);
+    }
+}
+
+// Resident work-groups per CU of a kernel at a dynamic LDS size (cached: the
+// occupancy query is host work).
+int groups_per_cu(const void *fn, size_t lds) {
+    struct Entry {
+        const void *fn;
+        size_t lds;
+        int n;
+    };
+    thread_local Entry cache[8] = {};
+    thread_local int next = 0;
+    for (const Entry &e : cache)
+        if (e.fn == fn && e.lds == lds && e.n > 0) return e.n;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, lds) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = 1;
+    }
+    cache[next] = {fn, lds, n};
+    next = (next + 1) % 8;
+    return n;
+}
+
+template <int kDepth, bool kAccum>
+hipError_t launch_kernel(LaunchParams p, hipStream_t stream) {
+    const size_t lds = lds_bytes(p);
+    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
+    dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY - 1) / kTileY, p.n_views);
+    const int wave_tiles = ((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
+    const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
+    if (kQueuedDepth(kDepth) && p.sched && p.n_views == 1 && wave_tiles > resident * (kThreads / 64)) {
+        grid = dim3(resident, 1, 1);  // queued: more wave tiles than resident waves
+    } else {
+        p.sched = nullptr;
+    }
+    hipLaunchKernelGGL((render_kernel<kDepth, kAccum>), grid, dim3(kThreads), lds, stream, p);
+    return hipGetLastError();
+}
+
 template <int kDepth>
 hipError_t launch_depth(const LaunchParams &p, hipStream_t stream) {
-    const dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY - 1) / kTileY, p.n_views);
-    if (p.spp > 0)
-        hipLaunchKernelGGL((render_kernel<kDepth, true>), grid, dim3(kThreads), lds_bytes(p), stream, p);
-    else
-        hipLaunchKernelGGL((render_kernel<kDepth, false>), grid, dim3(kThreads), lds_bytes(p), stream, p);
-    return hipGetLastError();
+    return p.spp > 0 ? launch_kernel<kDepth, true>(p, stream) : launch_kernel<kDepth, false>(p, stream);
 }
 
 }  // namespace

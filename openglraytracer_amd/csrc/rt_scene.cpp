@@ -489,19 +489,54 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         r.reflectivity = mats[m].reflectivity;
         r.transparency = mats[m].transparency;
         r.refraction_index = mats[m].refraction_index;
-        for (int j = 0; j < n_lights; ++j)
+        // tame: every product finite and shininess in (0, 1e6): then the
+        // diffuse factor max(cos, 0) <= 1 + 2^-20 and pow(max(cos, 0),
+        // shininess) are finite (pow is skipped for a zero base; its exp2
+        // argument stays below 128 for such bases and exponents) and a light
+        // whose products are zero, or whose factor is zero, adds only +-0 to
+        // the sums (which start at +0 and so are never -0): its shadow ray
+        // cannot change the colour.
+        bool tame = mats[m].shininess > 0.0f && mats[m].shininess < 1e6f;
+        for (int j = 0; j < n_lights; ++j) {
+            LightMatRec &q = lm[m * n_lights + j];
             for (int k = 0; k < 4; ++k) {
-                lm[m * n_lights + j].ld_md[k] = lights[j].diffuse[k] * mats[m].diffuse[k];   // :830
-                lm[m * n_lights + j].ls_ms[k] = lights[j].specular[k] * mats[m].specular[k];  // :832
+                q.ld_md[k] = lights[j].diffuse[k] * mats[m].diffuse[k];   // :830
+                q.ls_ms[k] = lights[j].specular[k] * mats[m].specular[k];  // :832
+                q.d_nz |= q.ld_md[k] != 0.0f;
+                q.s_nz |= q.ls_ms[k] != 0.0f;
+                tame = tame && std::isfinite(q.ld_md[k]) && std::isfinite(q.ls_ms[k]);
             }
+        }
+        for (int j = 0; j < n_lights; ++j) lm[m * n_lights + j].always = tame ? 0 : 1;
     }
+    // Shadow culling cones of every (light, sphere) pair (float64; culling
+    // only, the margins dwarf the float32 rounding of the stored values).
+    std::vector<ShadowCone> cones(static_cast<size_t>(n_lights) * sph.size());
+    for (int j = 0; j < n_lights; ++j)
+        for (size_t s = 0; s < sph.size(); ++s) {
+            ShadowCone &c = cones[j * sph.size() + s];
+            const double v[3] = {double(sph[s].cx) - lights[j].position[0], double(sph[s].cy) - lights[j].position[1],
+                                 double(sph[s].cz) - lights[j].position[2]};
+            const double d = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+            const double rp = double(smeta[s].radius) + 0.021 + 1e-3 * d;
+            if (!(std::isfinite(d) && std::isfinite(rp)) || d <= rp) {
+                c.near = 1.0f;  // always a candidate
+                continue;
+            }
+            for (int r = 0; r < 3; ++r) c.v[r] = static_cast<float>(v[r] / d);
+            c.far = static_cast<float>(d - rp);
+            const double sp = rp / d;
+            c.sph = static_cast<float>(sp);
+            c.cph = static_cast<float>(std::sqrt(std::max(0.0, 1.0 - sp * sp)));
+        }
     // A light with zero diffuse and specular colour (the reference's ambient
     // light, :202-207) adds +-0 to the sums for every finite material with
     // shininess >= 0 (pow then stays finite), so lit and shadowed agree and
     // the kernel may skip it; its ambient term is in amb_sum.
     bool materials_tame = true;
     for (int m = 0; m < n_mats; ++m) {
-        materials_tame = materials_tame && mats[m].shininess >= 0.0f;
+        // (shininess below 1e6 keeps pow's exp2 argument below 128: finite)
+        materials_tame = materials_tame && mats[m].shininess >= 0.0f && mats[m].shininess < 1e6f;
         for (int k = 0; k < 4; ++k)
             materials_tame = materials_tame && std::isfinite(mats[m].diffuse[k]) && std::isfinite(mats[m].specular[k]);
     }
@@ -521,6 +556,19 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     ds.off_lights = off;  off += units(lrec.size() * sizeof(LightRec));
     ds.off_lightmat = off; off += units(lm.size() * sizeof(LightMatRec));
     ds.off_bvh = off;     off += units(bvh.size() * sizeof(BvhNode));
+    // The cone table rides in LDS only while the work-group's LDS stays small
+    // enough for full occupancy (config 4's 256 spheres x 3 lights would add
+    // 24 KB and cut the resident work-groups per CU); without it the kernel
+    // derives the cones per wave (off_cone = -1).
+    const size_t per_frame = sph.size() * 32 + boxes.size() * 16;
+    const size_t with_cones = (static_cast<size_t>(off) + units(cones.size() * sizeof(ShadowCone))) * 16 + per_frame;
+    if (with_cones <= kConeLdsBudget) {
+        ds.off_cone = off;
+        off += units(cones.size() * sizeof(ShadowCone));
+    } else {
+        ds.off_cone = -1;
+        cones.clear();
+    }
     ds.n_bvh = static_cast<int32_t>(bvh.size());
     ds.blob_units = off;
     ds.n_spheres = static_cast<int32_t>(sph.size());
@@ -538,6 +586,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     put(ds.off_lights, lrec.data(), lrec.size() * sizeof(LightRec));
     put(ds.off_lightmat, lm.data(), lm.size() * sizeof(LightMatRec));
     put(ds.off_bvh, bvh.data(), bvh.size() * sizeof(BvhNode));
+    if (ds.off_cone >= 0) put(ds.off_cone, cones.data(), cones.size() * sizeof(ShadowCone));
     return RT_OK;
 }
 

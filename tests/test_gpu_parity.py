@@ -299,6 +299,54 @@ def test_monte_carlo_matches_oracle(gpu_ctx):
     sc.close()
 
 
+def test_queued_distribution_edge_scene(gpu_ctx):
+    """Depth >= 2 frames with more 8x8 wave tiles than resident waves run on
+    the queued (resident-grid, atomic wave-tile queue) path: the edge scene of
+    test_mixed_edge_scene at 800x512 (6400 wave tiles), bands against the
+    oracle, rendered repeatedly (the queue counters reset themselves)."""
+    cam = rt.reference_camera(0.0)
+    cx, cy, cz = cam.position
+    objs = [scenes.sphere((cx, cy, cz), 0.5, rt.abi.RED_GLASS), scenes.room_box(),
+            scenes.box((-1, -1, -1), (1, 1, 1), (2, 1, 0), (10, 20, 30), rt.abi.MIRROR),
+            scenes.sphere((0, 0, 0), 2.0, rt.abi.MATERIAL1), scenes.sphere((0, 0, 0), 2.0, rt.abi.MATERIAL2),
+            scenes.box((-5, -5, -0.01), (5, 5, 0.01), (0, 0, -2), (5, 30, 60), rt.abi.GREEN_GLASS)]
+    objs += scenes.bench_objects(24, seed=9)[1:]
+    w, h, depth = 800, 512, 3
+    view = rt.make_view(None, 0.0)
+    sc = rt.Scene(gpu_ctx, objs)
+    frames = []
+    for _ in range(3):
+        out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_device(gpu_ctx, sc, out.data_ptr(), w, h, depth, view=view)
+        torch.cuda.synchronize()
+        frames.append(out.cpu().numpy())
+    sc.close()
+    assert all(np.array_equal(frames[0], f, equal_nan=True) for f in frames[1:])
+    for r0, r1 in [(0, 6), (250, 262), (506, 512)]:
+        o = oracle_render(objs, w, h, depth, rows=(r0, r1))
+        assert np.array_equal(frames[0][r0:r1], o, equal_nan=True), (r0, parity_stats(frames[0][r0:r1], o))
+
+
+def test_concurrent_streams_share_a_context(gpu_ctx):
+    """Launches in flight on two streams of one context (queued frames use a
+    counter slot per launch) give the frames a synchronous render gives."""
+    objs = scenes.bench_objects(40, seed=2)
+    w, h, depth = 1024, 512, 2
+    view_a, view_b = rt.make_view(None, 0.0), rt.make_view(None, 0.5)
+    sc = rt.Scene(gpu_ctx, objs)
+    ref_a = rt.render(gpu_ctx, sc, w, h, depth, view=view_a)
+    ref_b = rt.render(gpu_ctx, sc, w, h, depth, view=view_b)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(6)]
+    for k, out in enumerate(outs):
+        s, v = (sa, view_a) if k % 2 == 0 else (sb, view_b)
+        rt.render_device(gpu_ctx, sc, out.data_ptr(), w, h, depth, view=v, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for k, out in enumerate(outs):
+        assert np.array_equal(out.cpu().numpy(), ref_a if k % 2 == 0 else ref_b), k
+    sc.close()
+
+
 def test_scene_update_animation(gpu_ctx):
     """rt_scene_update: the shipped scene animated over frames, one scene object."""
     sc = rt.Scene(gpu_ctx, rt.reference_objects(0.0))

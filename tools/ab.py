@@ -1,0 +1,91 @@
+"""Interleaved A/B timing of several builds in ONE process (development probe).
+
+    python tools/ab.py CONFIG[,CONFIG...] BUILD [BUILD ...]
+
+BUILD is a directory under tools/_ablate (tools/ablate.sh) or "main" for the
+in-tree library. Every build gets its own context and scene; each round times
+every build once (one event pair around REPS back-to-back launches on a
+non-default stream), rounds interleaved so clock drift hits all builds alike.
+Prints the median and min per-frame kernel time and a hash of the frame.
+"""
+import ctypes as C
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch
+import openglraytracer_amd as rt
+from oracle import scenes
+
+cfgs = sys.argv[1].split(",")
+builds = sys.argv[2:]
+ROUNDS = 7
+
+
+def load(name):
+    path = rt.LIB_PATH if name == "main" else os.path.join(ROOT, "tools", "_ablate", name, "libopenglraytracer_amd.so")
+    L = C.CDLL(path)
+    vp, i = C.c_void_p, C.c_int
+    L.rt_create.argtypes = [i, vp]
+    L.rt_scene_create.argtypes = [vp, vp, i, vp, i, vp, i, vp]
+    L.rt_scene_destroy.argtypes = [vp]
+    L.rt_context_set.argtypes = [vp, i, i]
+    L.rt_render_view.argtypes = [vp, vp, vp, i, i, i, i, i, vp, i, vp]
+    ctx = C.c_void_p()
+    assert L.rt_create(0, C.byref(ctx)) == 0
+    L.rt_context_set(ctx, rt.abi.RT_OPT_TIMING, 0)
+    return L, ctx
+
+
+libs = {b: load(b) for b in builds}
+stream = torch.cuda.Stream()
+torch.cuda.set_stream(stream)
+mats = rt.reference_materials()
+lights = rt.reference_lights()
+view = rt.make_view(None, 0.0)
+for cfg in cfgs:
+    build, w, h, depth = scenes.CONFIGS[cfg]
+    objs = build()
+    oa = (rt.Object * len(objs))(*objs)
+    ma = (rt.Material * len(mats))(*mats)
+    la = (rt.Light * len(lights))(*lights)
+    out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+    reps = 20 if w * h <= 2_100_000 else (4 if w * h <= 8_300_000 else 1)
+    state = {}
+    for b, (L, ctx) in libs.items():
+        sc = C.c_void_p()
+        assert L.rt_scene_create(ctx, oa, len(objs), ma, len(mats), la, len(lights), C.byref(sc)) == 0
+        state[b] = sc
+    times = {b: [] for b in builds}
+    digests = {}
+
+    def launch(b):
+        L, ctx = libs[b]
+        rc = L.rt_render_view(ctx, state[b], C.byref(view), w, h, depth, 0, h, C.c_void_p(out.data_ptr()), 1,
+                              C.c_void_p(stream.cuda_stream))
+        assert rc == 0, rc
+
+    for b in builds:  # warm-up + frame hash
+        launch(b)
+        torch.cuda.synchronize()
+        digests[b] = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
+    for _ in range(ROUNDS):
+        for b in builds:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            launch(b)
+            e0.record(stream)
+            for _ in range(reps):
+                launch(b)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[b].append(e0.elapsed_time(e1) / reps)
+    for b in builds:
+        t = np.array(times[b])
+        print("%-8s %-10s median %.4f ms  min %.4f ms  frame %s" % (cfg, b, np.median(t), t.min(), digests[b]),
+              flush=True)
+    for b, (L, ctx) in libs.items():
+        L.rt_scene_destroy(state[b])

@@ -20,7 +20,8 @@ cfgs = sys.argv[2:] or ["config2"]
 rt.LIB_PATH = os.path.join(ROOT, "tools", "_ablate", name, "libopenglraytracer_amd.so")
 ctx = rt.Context(0)
 view = rt.make_view(None, 0.0)
-stream = torch.cuda.current_stream()
+stream = torch.cuda.Stream()  # non-default: the C-ABI runs NULL-stream calls synchronously
+torch.cuda.set_stream(stream)
 for cfg in cfgs:
     build, w, h, depth = scenes.CONFIGS[cfg]
     sc = rt.Scene(ctx, build())
