@@ -806,37 +806,6 @@ __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     return (blk * p.n_shards + p.shard) * p.block_rows + (local - blk * p.block_rows);
 }
 
-// Conservative pixel footprint of a sphere: project the 8 corners of its
-// (inflated) bounding cube with proj*view; valid only when the whole cube is
-// in front of the camera. Two pixels of margin on every side.
-__device__ int4 sphere_footprint(const LaunchParams &p, const FrameView &V, float4 c, float rad) {
-    const int4 all = make_int4(INT_MIN / 2, INT_MAX / 2, INT_MIN / 2, INT_MAX / 2);
-    const int hw = p.width / 2, hh = p.height / 2;
-    if (!V.cull || hw <= 0 || hh <= 0) return all;
-    const float r = rad * 1.001f + 1e-3f;
-    const float *P = V.proj;
-    float x0 = __builtin_inff(), x1 = -__builtin_inff(), y0 = x0, y1 = x1;
-    bool ok = r == r && c.x == c.x && c.y == c.y && c.z == c.z;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const float X = c.x + ((i & 1) ? r : -r), Y = c.y + ((i & 2) ? r : -r), Z = c.z + ((i & 4) ? r : -r);
-        const float cw = P[3] * X + P[7] * Y + P[11] * Z + P[15];
-        const float cx = P[0] * X + P[4] * Y + P[8] * Z + P[12];
-        const float cy = P[1] * X + P[5] * Y + P[9] * Z + P[13];
-        ok = ok && cw > 1e-4f;
-        const float iw = __builtin_amdgcn_rcpf(cw);  // 2-pixel margin >> its error
-        x0 = fminf(x0, cx * iw); x1 = fmaxf(x1, cx * iw);
-        y0 = fminf(y0, cy * iw); y1 = fmaxf(y1, cy * iw);
-    }
-    // pixel x <-> NDC (x - hw) / hw (:377)
-    const float fx0 = floorf(x0 * hw + hw) - 2.0f, fx1 = ceilf(x1 * hw + hw) + 2.0f;
-    const float fy0 = floorf(y0 * hh + hh) - 2.0f, fy1 = ceilf(y1 * hh + hh) + 2.0f;
-    const float lim = 1.0e9f;
-    ok = ok && fabsf(fx0) < lim && fabsf(fx1) < lim && fabsf(fy0) < lim && fabsf(fy1) < lim;
-    if (!ok) return all;
-    return make_int4(static_cast<int>(fx0), static_cast<int>(fx1), static_cast<int>(fy0), static_cast<int>(fy1));
-}
-
 // Counter-based sample jitter (Monte-Carlo extension):
 // a 32-bit integer hash of (seed, sample, pixel, axis); u in [0, 1) with 24
 // bits. Integer-only, so the oracle reproduces it exactly.
@@ -863,43 +832,129 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #define RT_WAVES_PER_EU(d) ((d) >= 2 ? 6 : 1)
 #endif
 #define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(kDepth))))
-// Per-frame constants of one view into LDS: the camera-origin terms of every
-// sphere (oc, qc :587-588) and box (local origin :655, strictly-inside flag)
-// and every sphere's conservative pixel footprint.
-__device__ __forceinline__ void frame_setup(const LaunchParams &p, const FrameView &V, const float4 *lds,
-                                            float4 *sph_cam, int4 *sph_px, float4 *box_cam) {
+// Reductions over aligned groups of 8 lanes (DPP: quad butterflies, then the
+// half-row mirror); every lane of the group ends with the result.
+__device__ __forceinline__ float group8_min(float v) {
+    v = fminf(v, dpp<0xB1, 0xF>(v));
+    v = fminf(v, dpp<0x4E, 0xF>(v));
+    return fminf(v, dpp<0x141, 0xF>(v));
+}
+__device__ __forceinline__ float group8_max(float v) {
+    v = fmaxf(v, dpp<0xB1, 0xF>(v));
+    v = fmaxf(v, dpp<0x4E, 0xF>(v));
+    return fmaxf(v, dpp<0x141, 0xF>(v));
+}
+
+// Per-frame constants of one view, written to LDS: the camera-origin terms of
+// every sphere (oc, qc :587-588) and box (local origin :655, strictly-inside
+// flag) and every sphere's conservative pixel footprint. Reads the scene from
+// the device blob (not from its LDS copy), so it needs no barrier after the
+// staging; a sphere's footprint is spread over 8 lanes, one corner of its
+// bounding cube each (group-of-8 DPP min / max), to keep the prologue short.
+__device__ __forceinline__ void frame_setup(const LaunchParams &p, const FrameView &V, float4 *sph_cam,
+                                            int4 *sph_px, float4 *box_cam) {
+    const float4 *blob = static_cast<const float4 *>(p.scene);
     const v3 origin = mk(V.origin[0], V.origin[1], V.origin[2]);
-    const float4 *sph = lds + p.off_spheres;
-    const int4 *smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
+    const int hw = p.width / 2, hh = p.height / 2;
+    const bool cull = V.cull && hw > 0 && hh > 0;
+    const float *P = V.proj;
 #ifdef RT_ABLATE_SETUP
-    if (p.n_spheres < 0)
+    if (p.n_spheres >= 0) return;
 #endif
-    for (int s = threadIdx.x; s < p.n_spheres; s += kThreads) {
-        const float4 c = sph[s];
-        const v3 oc = sub(origin, mk(c.x, c.y, c.z));
-        sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);
-        sph_px[s] = sphere_footprint(p, V, c, __int_as_float(smeta[s].z));
+    for (int item = threadIdx.x; item < 8 * p.n_spheres; item += kThreads) {  // whole groups of 8 lanes
+        const int s = item >> 3, i = item & 7;
+        const float4 c = blob[p.off_spheres + s];
+        const float rad = __int_as_float(reinterpret_cast<const int4 *>(blob + p.off_smeta)[s].z);
+        // corner i of the (inflated) bounding cube, projected with proj*view
+        const float r = rad * 1.001f + 1e-3f;
+        const float X = c.x + ((i & 1) ? r : -r), Y = c.y + ((i & 2) ? r : -r), Z = c.z + ((i & 4) ? r : -r);
+        const float cw = P[3] * X + P[7] * Y + P[11] * Z + P[15];
+        const float cx = P[0] * X + P[4] * Y + P[8] * Z + P[12];
+        const float cy = P[1] * X + P[5] * Y + P[9] * Z + P[13];
+        const float iw = __builtin_amdgcn_rcpf(cw);  // 2-pixel margin >> its error
+        const bool ok_i = cw > 1e-4f && r == r && c.x == c.x && c.y == c.y && c.z == c.z;
+        const float x0 = group8_min(cx * iw), x1 = group8_max(cx * iw);
+        const float y0 = group8_min(cy * iw), y1 = group8_max(cy * iw);
+        const bool ok = group8_min(ok_i ? 1.0f : 0.0f) == 1.0f;  // every corner in front of the camera
+        if (i == 0) {
+            const v3 oc = sub(origin, mk(c.x, c.y, c.z));
+            sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);
+            // pixel x <-> NDC (x - hw) / hw (:377); two pixels of margin
+            const float fx0 = floorf(x0 * hw + hw) - 2.0f, fx1 = ceilf(x1 * hw + hw) + 2.0f;
+            const float fy0 = floorf(y0 * hh + hh) - 2.0f, fy1 = ceilf(y1 * hh + hh) + 2.0f;
+            const float lim = 1.0e9f;
+            const bool fin = fabsf(fx0) < lim && fabsf(fx1) < lim && fabsf(fy0) < lim && fabsf(fy1) < lim;
+            sph_px[s] = cull && ok && fin ? make_int4(static_cast<int>(fx0), static_cast<int>(fx1),
+                                                      static_cast<int>(fy0), static_cast<int>(fy1))
+                                          : make_int4(INT_MIN / 2, INT_MAX / 2, INT_MIN / 2, INT_MAX / 2);
+        }
     }
-    const BoxRec *box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
+    const BoxRec *box = reinterpret_cast<const BoxRec *>(blob + p.off_boxes);
     for (int b = threadIdx.x; b < p.n_boxes; b += kThreads) {
         const v3 rs = xform_point(box[b].w2l, origin);
         box_cam[b] = make_float4(rs.x, rs.y, rs.z, strictly_inside(box[b], rs) ? 1.0f : 0.0f);
     }
 }
 
-// One 8x8 wave tile (wx, wy) of view z: lane l renders pixel (8 wx + l % 8, 8 wy + l / 8).
+// The pixel of lane `lane` in wave tile (wx, wy): frame column x, local row
+// (row of the launch's output) and frame row y (:327-329).
+struct Pixel {
+    int x, local_row, y;
+    bool active;
+};
+__device__ __forceinline__ Pixel wave_pixel(const LaunchParams &p, int wx, int wy) {
+    const int lane = threadIdx.x & 63;
+    Pixel px;
+    px.x = wx * 8 + (lane & 7);
+    px.local_row = wy * 8 + (lane >> 3);
+    px.active = px.x < p.width && px.local_row < p.n_rows;
+    px.y = output_row(p, px.active ? px.local_row : wy * 8);
+    return px;
+}
+
+// Camera ray through pixel (x, y) offset by (jx, jy) (:377-392); jx = jy = 0
+// for the reference's one ray per pixel (float(x - hw) + 0.0f is exact).
+__device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView &V, int x, int y, float jx,
+                                          float jy) {
+    const int hw = p.width / 2, hh = p.height / 2;
+    const float *M = V.unproj;  // column-major
+    // x - hw + jx is +0 or a multiple of 2^-24 of magnitude <= 2^16: the
+    // short division by the (uniform) W/2, H/2 >= 1 is the correctly rounded
+    // one (a 1-pixel-wide or -high frame divides by 0: IEEE path)
+    const float nx = static_cast<float>(x - hw) + jx, ny = static_cast<float>(y - hh) + jy;
+    float vx, vy;
+    if (hw > 0 && hh > 0) {
+        vx = div_r(nx, rcp_refined(static_cast<float>(hw)));
+        vy = div_r(ny, rcp_refined(static_cast<float>(hh)));
+    } else {
+        vx = nx / static_cast<float>(hw);
+        vy = ny / static_cast<float>(hh);
+    }
+    float ws[4], we[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        ws[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 0.5f + M[12 + k] * 1.0f;
+        we[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 1.0f + M[12 + k] * 1.0f;
+    }
+    const v3 s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
+    const v3 e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
+    Ray ray;
+    ray.start = mk(V.origin[0], V.origin[1], V.origin[2]);
+    ray.dir = normalize(sub(e3, s3));
+    return ray;
+}
+
+// One 8x8 wave tile (wx, wy) of view z: lane l renders pixel (8 wx + l % 8,
+// 8 wy + l / 8). `pre`: the lane's camera ray, already computed (the tiled
+// path computes it while the scene is staged), or nullptr.
 template <int kDepth, bool kAccum>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
-                                                 int z) {
-    const v3 origin = mk(V.origin[0], V.origin[1], V.origin[2]);
+                                                 int z, const Pixel &px, const Ray *pre) {
     S.cull = V.cull;
-    const int lane = threadIdx.x & 63;
-    const int x = wx * 8 + (lane & 7);
+    if (!__any(px.active)) return;
+    const int x = px.x, y = px.y, local_row = px.local_row;
+    const bool active = px.active;
     const int lr0 = wy * 8;
-    const int local_row = lr0 + (lane >> 3);
-    const bool active = x < p.width && local_row < p.n_rows;
-    if (!__any(active)) return;
-    const int y = output_row(p, active ? local_row : lr0);
     S.tx0 = wx * 8;
     S.tx1 = S.tx0 + 7;
     S.ty0 = INT_MAX;
@@ -909,45 +964,11 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         S.ty0 = fy < S.ty0 ? fy : S.ty0;
         S.ty1 = fy > S.ty1 ? fy : S.ty1;
     }
-
-    // ---- camera ray (:377-392) ----
-    const int hw = p.width / 2, hh = p.height / 2;
-    const float *M = V.unproj;  // column-major
-    // jx, jy: sub-pixel offsets of a Monte-Carlo sample (0 for the
-    // reference's one ray per pixel; float(x - hw) + 0.0f is exact)
-    // x - hw + jx is +0 or a multiple of 2^-24 of magnitude <= 2^16: the
-    // short division by the (uniform) W/2, H/2 >= 1 is the correctly rounded
-    // one (a 1-pixel-wide or -high frame divides by 0: IEEE path)
-    const Rcp rw = rcp_refined(static_cast<float>(hw)), rh = rcp_refined(static_cast<float>(hh));
-    const bool halves_ok = hw > 0 && hh > 0;
-    auto camera_ray = [&](float jx, float jy) {
-        const float nx = static_cast<float>(x - hw) + jx, ny = static_cast<float>(y - hh) + jy;
-        float vx, vy;
-        if (halves_ok) {
-            vx = div_r(nx, rw);
-            vy = div_r(ny, rh);
-        } else {
-            vx = nx / static_cast<float>(hw);
-            vy = ny / static_cast<float>(hh);
-        }
-        float ws[4], we[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            ws[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 0.5f + M[12 + k] * 1.0f;
-            we[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 1.0f + M[12 + k] * 1.0f;
-        }
-        const v3 s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
-        const v3 e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
-        Ray ray;
-        ray.start = origin;
-        ray.dir = normalize(sub(e3, s3));
-        return ray;
-    };
     float4 *out = p.out + static_cast<size_t>(z) * p.n_rows * p.width;
     const size_t idx = static_cast<size_t>(local_row) * p.width + x;
 
     if constexpr (!kAccum) {
-        const Ray ray = camera_ray(0.0f, 0.0f);
+        const Ray ray = pre ? *pre : camera_ray(p, V, x, y, 0.0f, 0.0f);
 #if defined(RT_ABLATE_RAYGEN)
         const v3 col = mk(float(x), float(y), 0.0f);
 #elif defined(RT_ABLATE_TRACE)
@@ -966,8 +987,8 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
             const float jx = p.jitter ? jitter_u(p.seed, sid, pixel, 0u) : 0.0f;
             const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
             v3 col;
-            if constexpr (kDepth == 0) col = trace0(S, camera_ray(jx, jy), active);
-            else col = trace_tree<kDepth>(S, camera_ray(jx, jy), active);
+            if constexpr (kDepth == 0) col = trace0(S, camera_ray(p, V, x, y, jx, jy), active);
+            else col = trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active);
             acc = add(acc, col);
         }
         if (active) {
@@ -1002,17 +1023,30 @@ constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 template <int kDepth, bool kAccum>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    // ---- stage the scene blob into LDS (one pass per work-group) ----
-    const float4 *blob = static_cast<const float4 *>(p.scene);
-    for (int i = threadIdx.x; i < p.blob_units; i += kThreads) lds[i] = blob[i];
-    float4 *sph_cam = lds + p.blob_units;
-    int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
-    float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
-    __syncthreads();
     const bool queued = kQueuedDepth(kDepth) && p.sched != nullptr;
     const int z = queued ? 0 : static_cast<int>(blockIdx.z);
     const FrameView &V = p.view[z];
-    frame_setup(p, V, lds, sph_cam, sph_px, box_cam);
+    // wave index through readfirstlane: provably wave-uniform to the compiler,
+    // so the tile coordinates and culling rectangles stay in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // ---- prologue: stage the scene blob into LDS and derive the view's
+    // per-frame constants (both from the device blob, one barrier); the tiled
+    // path computes its camera rays while the staging loads are in flight ----
+    const float4 *blob = static_cast<const float4 *>(p.scene);
+    const int tid = threadIdx.x;
+    float4 first = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (tid < p.blob_units) first = blob[tid];
+    float4 *sph_cam = lds + p.blob_units;
+    int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
+    float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
+    const int own_wx = static_cast<int>(blockIdx.x) * kWavesX + wave % kWavesX;
+    const int own_wy = static_cast<int>(blockIdx.y) * kWavesY + wave / kWavesX;
+    const Pixel own = wave_pixel(p, own_wx, own_wy);
+    Ray own_ray;
+    if (!queued && !kAccum) own_ray = camera_ray(p, V, own.x, own.y, 0.0f, 0.0f);
+    if (tid < p.blob_units) lds[tid] = first;
+    for (int i = tid + kThreads; i < p.blob_units; i += kThreads) lds[i] = blob[i];
+    frame_setup(p, V, sph_cam, sph_px, box_cam);
     __syncthreads();
     Scene S;
     S.sph = lds + p.off_spheres;
@@ -1031,9 +1065,6 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.nb = p.n_boxes;
     S.nl = p.n_lights;
     S.nm = p.n_mats;
-    // wave index through readfirstlane: provably wave-uniform to the compiler,
-    // so the tile coordinates and culling rectangles stay in SGPRs
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int wtx = (p.width + 7) / 8;
     const int total = queued ? wtx * ((p.n_rows + 7) / 8) : 1;
     const int g = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave;  // global wave
@@ -1049,9 +1080,9 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     while (t < total) {
         int nxt = 0;
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
-        const int wx = queued ? t % wtx : static_cast<int>(blockIdx.x) * kWavesX + wave % kWavesX;
-        const int wy = queued ? t / wtx : static_cast<int>(blockIdx.y) * kWavesY + wave / kWavesX;
-        render_wave_tile<kDepth, kAccum>(p, S, V, wx, wy, z);
+        const int wx = queued ? t % wtx : own_wx, wy = queued ? t / wtx : own_wy;
+        render_wave_tile<kDepth, kAccum>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
+                                         (queued || kAccum) ? nullptr : &own_ray);
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
     if (!queued) return;
