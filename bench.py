@@ -7,10 +7,12 @@ materials, max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405
 A step renders N frames of 1920x1080 (N = number of GPUs; frame k is the
 reference orbit camera at time k/60 s). Every frame is row-tiled across the N
 ranks in interleaved 8-row blocks; each rank renders its blocks of all N
-frames in one launch (rt_render_batch), and rank 0 assembles the N frames with
-one RCCL gather over xGMI plus a row de-interleave. Per-GPU work is one frame
-per step at every N: weak scaling. At N=1 a step is one full frame rendered
-in place (no collective).
+frames in one launch (rt_render_batch), and one RCCL all-to-all over xGMI
+gathers frame k to rank k (N gathers at once, every link carrying 1/N of the
+frame traffic), which de-interleaves its rows into the assembled frame. The
+exchange of step i runs on its own stream beside the render of step i+1
+(double-buffered). Per-GPU work is one frame per step at every N: weak
+scaling. At N=1 a step is one full frame rendered in place (no collective).
 
 --workload config5 (a Monte-Carlo extension the
 reference does not have): one step = the 1920x1080 frame at 1024 jittered
@@ -119,28 +121,35 @@ def main():
 
     ctx = rt.Context(device)
     scene = rt.Scene(ctx, rt.bench_objects(N_SPHERES, 0))
-    # a stream of our own, made current: the render launches, the events and
-    # the collectives are ordered on it and the launches are asynchronous (the
-    # C-ABI treats a NULL stream — torch's default stream handle is 0 — as
-    # "synchronous on the context's stream", like glFinish)
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    sh = stream.cuda_stream
+    ctx.set_timing(False)  # no per-launch markers of the library's own
+    # Streams of our own: renders are launched asynchronously on `render_s`
+    # (the C-ABI treats a NULL stream — torch's default stream handle is 0 —
+    # as "synchronous on the context's stream", like glFinish); the current
+    # stream `comm_s` orders the collectives (RCCL runs on its own stream
+    # behind it) and the frame assembly.
+    render_s = torch.cuda.Stream()
+    comm_s = torch.cuda.Stream()
+    torch.cuda.set_stream(comm_s)
+    sh = render_s.cuda_stream
     assert sh, "need a non-default HIP stream"
-
     mc = args.workload == "config5"
 
     if not mc:
+        # N frames in flight, frame k = the orbit camera at t = k/60 s; every
+        # rank renders its interleaved 8-row blocks of all N frames in one
+        # launch (rt_render_batch); one all-to-all hands frame k's rows to
+        # rank k (N gathers at once), which de-interleaves its frame. Double
+        # buffered: the exchange of step i overlaps the render of step i+1.
         n_frames = world
         views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
-        # every launch renders this rank's rows of all n_frames frames
-        # (rt_render_batch: blockIdx.z = frame); N=1 renders whole frames in place
         rows_mine = HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
-        flat_elems = frame.flat_shard_elems(n_frames, HEIGHT, WIDTH, BLOCK_ROWS, world)
-        buf = torch.zeros(flat_elems, dtype=torch.float32, device="cuda")
-        gathered = ([torch.empty(flat_elems, dtype=torch.float32, device=coll_dev) for _ in range(world)]
-                    if (world > 1 and rank == 0) else None)
-        perm = torch.as_tensor(frame.assembly_permutation(HEIGHT, BLOCK_ROWS, world), device=coll_dev)
+        bufs = [torch.zeros(n_frames * rows_mine * WIDTH * 4, dtype=torch.float32, device="cuda")
+                for _ in range(2 if world > 1 else 1)]
+        if world > 1:
+            in_splits, out_splits = frame.exchange_splits(HEIGHT, WIDTH, BLOCK_ROWS, world, rank)
+            recv = [torch.empty(sum(out_splits), dtype=torch.float32, device=coll_dev) for _ in bufs]
+            perm = torch.as_tensor(frame.assembly_permutation(HEIGHT, BLOCK_ROWS, world), device=coll_dev)
+            frames_out = [None, None]
         px_per_launch = WIDTH * rows_mine * n_frames
         rays_per_step = n_frames * WIDTH * HEIGHT
     else:
@@ -151,53 +160,70 @@ def main():
         px_per_launch = WIDTH * HEIGHT
         rays_per_step = MC_SPP * WIDTH * HEIGHT
 
-    # Kernel time from HIP events on the stream the kernel is launched on. At
-    # N=1 a step is exactly one render launch: one event pair brackets the K
-    # back-to-back launches of the timed region (no markers between frames).
-    # At N>1 a pair brackets every render launch (the collective runs between).
-    ctx.set_timing(False)  # no per-launch markers of the library's own
+    # Kernel time from HIP events on the render stream. At N=1 (config 2) a
+    # step is exactly one render launch: one event pair brackets the K
+    # back-to-back launches of the timed region (no markers between frames);
+    # otherwise a pair brackets every render launch.
     per_launch = world > 1 or mc
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps if per_launch else 1)]
+    rendered = [torch.cuda.Event() for _ in range(2)]
+    freed = [None, None]  # event: the exchange has finished reading bufs[slot]
 
     def step(timed, it=0):
-        if timed and per_launch:
-            ev[it][0].record(stream)
-        if not mc:
-            rt.render_batch(ctx, scene, buf.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS,
-                            world, rank, stream=sh)
-        else:
-            accum.zero_()
+        if mc:
+            accum.zero_()  # on comm_s: after the previous step's all-reduce read it
+            render_s.wait_stream(comm_s)
+            if timed:
+                ev[it][0].record(render_s)
             rt.render_accumulate(ctx, scene, accum.data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, spp_mine, sample0,
                                  seed=0, view=view, stream=sh)
-        if timed and per_launch:
-            ev[it][1].record(stream)
-        if not mc:
-            if world > 1:
-                dist.gather(buf if coll_dev == "cuda" else buf.cpu(), gathered, dst=0)
-                if rank == 0:  # (n_frames, H, W, 4) in frame row order
-                    frame.assemble(gathered, n_frames, HEIGHT, WIDTH, BLOCK_ROWS, perm=perm)
-        else:
-            total = accum
+            if timed:
+                ev[it][1].record(render_s)
+            comm_s.wait_stream(render_s)
             if world > 1:
                 total = accum if coll_dev == "cuda" else accum.cpu()
-                dist.all_reduce(total)
+                dist.all_reduce(total)  # RCCL: the partial sums of all ranks' samples
+            else:
+                total = accum
             if rank == 0:
                 total.mul_(1.0 / MC_SPP)  # the estimate: mean over all samples
+            return
+        if world == 1:  # one frame rendered in place, launches back to back
+            rt.render_batch(ctx, scene, bufs[0].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS, 1, 0,
+                            stream=sh)
+            return
+        slot = it % 2
+        if freed[slot] is not None:
+            render_s.wait_event(freed[slot])  # the exchange of step it-2 has read bufs[slot]
+        if timed:
+            ev[it][0].record(render_s)
+        rt.render_batch(ctx, scene, bufs[slot].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS, world,
+                        rank, stream=sh)
+        if timed:
+            ev[it][1].record(render_s)
+        rendered[slot].record(render_s)
+        comm_s.wait_event(rendered[slot])
+        src = bufs[slot] if coll_dev == "cuda" else bufs[slot].cpu()
+        dist.all_to_all_single(recv[slot], src, out_splits, in_splits)  # frame k's rows -> rank k
+        frames_out[slot] = frame.assemble_frame(recv[slot], HEIGHT, WIDTH, BLOCK_ROWS, world, perm=perm)
+        e = torch.cuda.Event()
+        e.record(comm_s)
+        freed[slot] = e
 
-    for _ in range(args.warmup):
-        step(False)
+    for i in range(args.warmup):
+        step(False, i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if not per_launch:
-        ev[0][0].record(stream)
+        ev[0][0].record(render_s)
     for it in range(args.steps):
         step(True, it)
     if not per_launch:
-        ev[0][1].record(stream)
+        ev[0][1].record(render_s)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -222,7 +248,9 @@ def main():
                                     "(primary + shadow rays)",
                         "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES, "max_depth": MAX_DEPTH,
                         "frames_per_step": n_frames, "row_block": BLOCK_ROWS,
-                        "parallelism": ("row-tiles x%d + RCCL gather" % world) if world > 1 else "single GPU"}
+                        "parallelism": ("row-tiles x%d + RCCL all-to-all frame exchange (frame k gathered to "
+                                        "rank k), overlapped with the next render" % world)
+                                       if world > 1 else "single GPU"}
         else:
             workload = {"workload": "config5: 1920x1080 x 1024 spp Monte-Carlo, room box + 16 spheres, "
                                     "max_depth 0", "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES,
