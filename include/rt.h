@@ -212,6 +212,16 @@ int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *
  * stream with the kernels alone (back-to-back launches, e.g. a benchmark
  * timing many frames with one event pair of its own). */
 #define RT_OPT_TIMING 2
+/* RT_OPT_OUTPUT (default RT_OUTPUT_RGBA32F): the surface format renders
+ * write. RT_OUTPUT_RGBA8 is the shipped app's GL_RGBA8 texture
+ * (OpenGLRaytracer/main.cpp:152-159, :223; raytrace_compute.glsl:404): the
+ * kernel packs each pixel in its epilogue — clamp to [0, 1], unorm rounding,
+ * exactly rt_pack_rgba8 of the float frame — and stores 4 bytes per pixel, so
+ * every `out` buffer then holds width*rows*4 bytes (uint8 r, g, b, a).
+ * rt_render_accumulate keeps float sums and refuses RGBA8. */
+#define RT_OPT_OUTPUT 3
+#define RT_OUTPUT_RGBA32F 0
+#define RT_OUTPUT_RGBA8 1
 int rt_context_set(rt_context *ctx, int option, int value);
 
 /* Kernel-only timing of the last render call (ms, from HIP events around the

@@ -194,6 +194,12 @@ class Context:
         """RT_OPT_TIMING: HIP events around every launch (for last_kernel_ms)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_TIMING, 1 if on else 0))
 
+    def set_output(self, fmt):
+        """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel) or
+        abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)."""
+        _check(lib().rt_context_set(self._h, abi.RT_OPT_OUTPUT, fmt))
+        self.output = fmt
+
     def last_kernel_ms(self):
         ms = C.c_float()
         _check(lib().rt_last_kernel_ms(self._h, C.byref(ms)))
@@ -250,6 +256,24 @@ def render(ctx, scene, width, height, max_depth=0, time=0.0, camera=None, view=N
         view = make_view(camera, time)
     _check(lib().rt_render_view(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
                                 r0, r1, out.ctypes.data, 0, None))
+    return out[: r1 - r0, :width]
+
+
+def render_rgba8(ctx, scene, width, height, max_depth=0, time=0.0, camera=None, view=None, rows=None):
+    """Render rows [r0, r1) as the shipped app's GL_RGBA8 surface: a host
+    array (r1-r0, width, 4) uint8, packed by the kernel's epilogue (equal to
+    pack_rgba8 of the float frame)."""
+    r0, r1 = rows if rows is not None else (0, height)
+    out = np.zeros((max(r1 - r0, 1), max(width, 1), 4), np.uint8)
+    if view is None:
+        view = make_view(camera, time)
+    prev = getattr(ctx, "output", abi.RT_OUTPUT_RGBA32F)
+    ctx.set_output(abi.RT_OUTPUT_RGBA8)
+    try:
+        _check(lib().rt_render_view(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
+                                    r0, r1, out.ctypes.data, 0, None))
+    finally:
+        ctx.set_output(prev)
     return out[: r1 - r0, :width]
 
 

@@ -20,6 +20,9 @@ RT_MAX_LIGHTS = 16
 RT_MAX_MATERIALS = 256
 RT_OPT_CULLING = 1
 RT_OPT_TIMING = 2
+RT_OPT_OUTPUT = 3
+RT_OUTPUT_RGBA32F = 0
+RT_OUTPUT_RGBA8 = 1
 RT_MAX_BATCH = 8
 
 # material indices of the reference table (raytrace_compute.glsl:74-157)

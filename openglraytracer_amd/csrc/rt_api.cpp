@@ -87,6 +87,7 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.off_lightmat = d.off_lightmat;
     p.off_bvh = d.off_bvh;
     p.off_cone = d.off_cone;
+    p.out_rgba8 = ctx->output == RT_OUTPUT_RGBA8 ? 1 : 0;
     p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
     return p;
@@ -270,6 +271,7 @@ int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, 
     p.n_rows = row_end - row_begin;
     const size_t n_px = static_cast<size_t>(p.n_rows) * width;
     hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
+    const size_t px_bytes = p.out_rgba8 ? 4 : sizeof(float4);
     if (out_is_device) {
         p.out = reinterpret_cast<float4 *>(out);
     } else {
@@ -277,7 +279,7 @@ int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, 
             if (ctx->staging) (void)hipFree(ctx->staging);
             ctx->staging = nullptr;
             ctx->staging_px = 0;
-            e = hipMalloc(&ctx->staging, n_px * sizeof(float4));
+            e = hipMalloc(&ctx->staging, n_px * sizeof(float4));  // sized for float: serves both formats
             if (e != hipSuccess) return hip_fail("hipMalloc(staging)", e);
             ctx->staging_px = n_px;
         }
@@ -286,7 +288,7 @@ int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, 
     rc = launch(ctx, p, max_depth, stream);
     if (rc != RT_OK) return rc;
     if (!out_is_device) {
-        e = hipMemcpyAsync(out, ctx->staging, n_px * sizeof(float4), hipMemcpyDeviceToHost, stream);
+        e = hipMemcpyAsync(out, ctx->staging, n_px * px_bytes, hipMemcpyDeviceToHost, stream);
         if (e != hipSuccess) return hip_fail("hipMemcpyAsync(out)", e);
     }
     if (!hip_stream) {
@@ -391,6 +393,10 @@ int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *
         set_error("rt_render_accumulate: bad view / accumulator / spp / row range");
         return RT_ERR_INVALID;
     }
+    if (ctx->output != RT_OUTPUT_RGBA32F) {
+        set_error("rt_render_accumulate: the accumulator is float (RT_OPT_OUTPUT must be RT_OUTPUT_RGBA32F)");
+        return RT_ERR_UNSUPPORTED;
+    }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail("hipSetDevice", e);
     LaunchParams p = base_params(ctx, scene, view, 1, width, height);
@@ -416,6 +422,13 @@ int rt_context_set(rt_context *ctx, int option, int value) {
     switch (option) {
         case RT_OPT_CULLING: ctx->culling = value ? 1 : 0; return RT_OK;
         case RT_OPT_TIMING: ctx->timing = value ? 1 : 0; return RT_OK;
+        case RT_OPT_OUTPUT:
+            if (value != RT_OUTPUT_RGBA32F && value != RT_OUTPUT_RGBA8) {
+                set_error("rt_context_set: unknown output format " + std::to_string(value));
+                return RT_ERR_INVALID;
+            }
+            ctx->output = value;
+            return RT_OK;
         default: set_error("rt_context_set: unknown option " + std::to_string(option)); return RT_ERR_INVALID;
     }
 }

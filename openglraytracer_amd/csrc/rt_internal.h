@@ -129,6 +129,7 @@ struct LaunchParams {
     // per tile.
     int32_t *sched;
     int32_t n_cu;
+    int32_t out_rgba8;  // 1: store GL_RGBA8 unorm bytes (uchar4 per pixel) instead of float4
 };
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
 constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
@@ -161,6 +162,7 @@ struct rt_context {
     bool timed = false;
     int culling = 1;  // RT_OPT_CULLING
     int timing = 1;   // RT_OPT_TIMING
+    int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int n_cu = 0;               // compute units of the device
     int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
     unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots

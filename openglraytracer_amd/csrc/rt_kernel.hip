@@ -806,6 +806,11 @@ __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     return (blk * p.n_shards + p.shard) * p.block_rows + (local - blk * p.block_rows);
 }
 
+__device__ __forceinline__ uint32_t unorm8(float v) {
+    v = v != v ? 0.0f : gmin(gmax(v, 0.0f), 1.0f);
+    return static_cast<uint32_t>(v * 255.0f + 0.5f);
+}
+
 // Counter-based sample jitter (Monte-Carlo extension):
 // a 32-bit integer hash of (seed, sample, pixel, axis); u in [0, 1) with 24
 // bits. Integer-only, so the oracle reproduces it exactly.
@@ -978,7 +983,16 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         if constexpr (kDepth == 0) col = trace0(S, ray, active);
         else col = trace_tree<kDepth>(S, ray, active);
 #endif
-        if (active) out[idx] = make_float4(col.x, col.y, col.z, 0.0f);
+        if (active) {
+            if (p.out_rgba8) {
+                // GL_RGBA8 unorm store of vec4(rgb, 0.0) (main.cpp:223, :404):
+                // clamp (NaN -> 0), v * 255 + 0.5, truncate — rt_pack_rgba8
+                reinterpret_cast<uint32_t *>(p.out)[static_cast<size_t>(z) * p.n_rows * p.width + idx] =
+                    unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16);
+            } else {
+                out[idx] = make_float4(col.x, col.y, col.z, 0.0f);
+            }
+        }
     } else {
         const uint32_t pixel = static_cast<uint32_t>(y) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x);
         v3 acc = mk(0.0f, 0.0f, 0.0f);

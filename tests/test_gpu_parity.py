@@ -361,3 +361,34 @@ def test_scene_update_animation(gpu_ctx):
     g = rt.render(gpu_ctx, sc, 64, 36, 1, view=rt.make_view(None, 0.0))
     assert np.array_equal(g, oracle_render(scenes.bench_objects(64), 64, 36, 1))
     sc.close()
+
+
+@pytest.mark.parametrize("cfg,w,h", [("shipped", 160, 90), ("config3", 256, 144)])
+def test_rgba8_surface_equals_packed_float_frame(gpu_ctx, cfg, w, h):
+    """RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 texture, main.cpp:152-159): the
+    kernel's packed epilogue == rt_pack_rgba8 of the float frame, bytewise;
+    shard / batch renders write 4 bytes per pixel too."""
+    if cfg == "shipped":
+        objs, depth = rt.reference_objects(0.0), 1
+    else:
+        build, _, _, depth = scenes.CONFIGS[cfg]
+        objs = build()
+    view = rt.make_view(None, 0.0)
+    sc = rt.Scene(gpu_ctx, objs)
+    f = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+    b = rt.render_rgba8(gpu_ctx, sc, w, h, depth, view=view)
+    assert np.array_equal(b, rt.pack_rgba8(f))
+    assert np.array_equal(rt.render_rgba8(gpu_ctx, sc, w, h, depth, view=view, rows=(7, 40)), b[7:40])
+    gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA8)
+    try:
+        out = torch.zeros((2, h, w, 4), dtype=torch.uint8, device="cuda")
+        rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, [view, view])
+        got = out.cpu().numpy()
+        assert np.array_equal(got[0], b) and np.array_equal(got[1], b)
+        acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+        with pytest.raises(rt.RTError) as e:
+            rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 1, view=view)
+        assert e.value.code == rt.abi.RT_ERR_UNSUPPORTED
+    finally:
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA32F)
+        sc.close()
