@@ -133,6 +133,18 @@ int rt_bench_objects(int n_spheres, uint64_t seed, rt_object *out);
 /* cam == NULL: the reference orbit camera at `time`. */
 int rt_make_view(const rt_camera *cam, float time, rt_view *out);
 
+/* Scene description input: the content the reference
+ * compiles into its shader (materials :74-157, lights :199-224, the animated
+ * objects :261-321 at `time`, the camera :334-364) read from JSON text —
+ * format in openglraytracer_amd/csrc/rt_scene_json.cpp. Fills the caller's
+ * arrays (capacities max_*; n_* = entries written); *has_camera = 1 when the
+ * text sets a camera (written to *cam, which may be NULL), else 0 (use the
+ * reference orbit camera). Host only; RT_ERR_INVALID with a message naming
+ * the problem (and the byte offset of a syntax error). */
+int rt_scene_desc_parse(const char *json, float time, rt_object *objs, int max_objs, int *n_objs,
+                        rt_material *mats, int max_mats, int *n_mats, rt_light *lights, int max_lights,
+                        int *n_lights, rt_camera *cam, int *has_camera);
+
 /* ---- device API ------------------------------------------------------ */
 int rt_create(int device, rt_context **out);
 void rt_destroy(rt_context *ctx);

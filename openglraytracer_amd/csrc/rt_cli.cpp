@@ -5,9 +5,11 @@
 // and writes each frame as PPM (what the RGBA8 surface shows) and/or PFM.
 //
 //   rt_cli [--width 1280] [--height 720] [--depth 0] [--time 0] [--frames 1]
-//          [--dt 0.016] [--scene shipped|spheres:N[:seed]] [--ppm out_%04d.ppm]
+//          [--dt 0.016] [--scene shipped|spheres:N[:seed]|FILE.json] [--ppm out_%04d.ppm]
 //          [--pfm out_%04d.pfm] [--device 0]
 #include <chrono>
+#include <fstream>
+#include <sstream>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -54,22 +56,44 @@ int main(int argc, char **argv) {
         else if (a == "--device") device = std::atoi(next());
         else {
             std::fprintf(stderr, "usage: rt_cli [--width W] [--height H] [--depth D] [--time T] [--frames K] "
-                                 "[--dt S] [--scene shipped|spheres:N[:seed]] [--ppm PAT] [--pfm PAT] [--device I]\n");
+                                 "[--dt S] [--scene shipped|spheres:N[:seed]|FILE.json] [--ppm PAT] [--pfm PAT] "
+                                 "[--device I]\n");
             return 2;
         }
     }
     rt_context *ctx = nullptr;
     if (rt_create(device, &ctx) != RT_OK) return fail("rt_create");
-    rt_material mats[RT_REFERENCE_MATERIALS];
-    rt_light lights[RT_REFERENCE_LIGHTS];
-    rt_reference_materials(mats);
-    rt_reference_lights(lights);
+    std::vector<rt_material> mats(RT_REFERENCE_MATERIALS);
+    std::vector<rt_light> lights(RT_REFERENCE_LIGHTS);
+    rt_reference_materials(mats.data());
+    rt_reference_lights(lights.data());
+    std::string json;  // a scene description file (rt_scene_desc_parse), re-read at every frame's time
+    if (scene.size() > 5 && scene.compare(scene.size() - 5, 5, ".json") == 0) {
+        std::ifstream f(scene);
+        if (!f) { std::fprintf(stderr, "rt_cli: cannot read %s\n", scene.c_str()); return 2; }
+        std::stringstream ss;
+        ss << f.rdbuf();
+        json = ss.str();
+    }
     std::vector<float> frame(static_cast<size_t>(width) * height * 4);
     rt_scene *sc = nullptr;
     for (int k = 0; k < frames; ++k) {
         const float t = time0 + k * dt;
         std::vector<rt_object> objs;
-        if (scene == "shipped") {
+        rt_camera cam;
+        int has_cam = 0;
+        if (!json.empty()) {
+            int no = 0, nm = 0, nl = 0;
+            objs.resize(RT_MAX_OBJECTS);
+            mats.resize(RT_MAX_MATERIALS);
+            lights.resize(RT_MAX_LIGHTS);
+            if (rt_scene_desc_parse(json.c_str(), t, objs.data(), RT_MAX_OBJECTS, &no, mats.data(), RT_MAX_MATERIALS,
+                                    &nm, lights.data(), RT_MAX_LIGHTS, &nl, &cam, &has_cam) != RT_OK)
+                return fail("rt_scene_desc_parse");
+            objs.resize(no);
+            mats.resize(nm);
+            lights.resize(nl);
+        } else if (scene == "shipped") {
             objs.resize(RT_REFERENCE_OBJECTS);
             rt_reference_objects(t, objs.data());
         } else if (scene.rfind("spheres:", 0) == 0) {
@@ -83,15 +107,18 @@ int main(int argc, char **argv) {
             return 2;
         }
         if (!sc) {
-            if (rt_scene_create(ctx, objs.data(), static_cast<int>(objs.size()), mats, RT_REFERENCE_MATERIALS,
-                                lights, RT_REFERENCE_LIGHTS, &sc) != RT_OK)
+            if (rt_scene_create(ctx, objs.data(), static_cast<int>(objs.size()), mats.data(),
+                                static_cast<int>(mats.size()), lights.data(), static_cast<int>(lights.size()),
+                                &sc) != RT_OK)
                 return fail("rt_scene_create");
-        } else if (rt_scene_update(ctx, sc, objs.data(), static_cast<int>(objs.size()), mats, RT_REFERENCE_MATERIALS,
-                                   lights, RT_REFERENCE_LIGHTS) != RT_OK) {
+        } else if (rt_scene_update(ctx, sc, objs.data(), static_cast<int>(objs.size()), mats.data(),
+                                   static_cast<int>(mats.size()), lights.data(), static_cast<int>(lights.size())) !=
+                   RT_OK) {
             return fail("rt_scene_update");
         }
         const auto t0 = std::chrono::steady_clock::now();
-        if (rt_render(ctx, sc, nullptr, t, width, height, depth, 0, height, frame.data(), 0, nullptr) != RT_OK)
+        if (rt_render(ctx, sc, has_cam ? &cam : nullptr, t, width, height, depth, 0, height, frame.data(), 0,
+                      nullptr) != RT_OK)
             return fail("rt_render");
         const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         float kms = 0.0f;

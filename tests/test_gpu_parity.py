@@ -392,3 +392,25 @@ def test_rgba8_surface_equals_packed_float_frame(gpu_ctx, cfg, w, h):
     finally:
         gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA32F)
         sc.close()
+
+
+def test_cli_renders_a_scene_description(gpu_ctx, tmp_path):
+    """rt_cli (the headless main()/draw() driver) on scenes/config1.json: its
+    PPM is the RGBA8 surface of the same frame rendered through the C-ABI."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "openglraytracer_amd", "rt_cli")
+    out = str(tmp_path / "f.ppm")
+    r = subprocess.run([cli, "--scene", os.path.join(root, "scenes", "config1.json"), "--width", "64",
+                        "--height", "48", "--depth", "1", "--ppm", out], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    objs, mats, lts, _ = rt.parse_scene(open(os.path.join(root, "scenes", "config1.json")).read())
+    sc = rt.Scene(gpu_ctx, objs, materials=mats, lights=lts)
+    f = rt.render(gpu_ctx, sc, 64, 48, 1, view=rt.make_view(None, 0.0))
+    sc.close()
+    data = open(out, "rb").read()
+    header = b"P6\n64 48\n255\n"
+    assert data.startswith(header)
+    img = np.frombuffer(data[len(header):], np.uint8).reshape(48, 64, 3)
+    assert np.array_equal(img, rt.pack_rgba8(f)[::-1, :, :3])  # PPM rows top-down

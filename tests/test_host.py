@@ -161,3 +161,67 @@ def test_ppm_and_pfm_dump(tmp_path):
     assert np.array_equal(f, img[..., :3])  # PFM rows are bottom-up, like GL
     with pytest.raises(rt.RTError):
         rt.write_ppm(str(tmp_path / "missing" / "x.ppm"), img)
+
+
+# ---- scene description input (rt_scene_desc_parse) ---------
+def as_bytes(records):
+    return [bytes(r) for r in records]
+
+
+@pytest.mark.parametrize("t", [0.0, 3.7])
+def test_scene_desc_defaults_are_the_reference_scene(t):
+    """'{}' and the shipped.json description are the shader's own scene at
+    `time` (raytrace_compute.glsl:74-157, :199-224, :261-321)."""
+    for text in ("{}", open(os.path.join(ROOT, "scenes", "shipped.json")).read()):
+        objs, mats, lts, cam = rt.parse_scene(text, t)
+        assert as_bytes(objs) == as_bytes(rt.reference_objects(t))
+        assert as_bytes(mats) == as_bytes(rt.reference_materials())
+        assert as_bytes(lts) == as_bytes(rt.reference_lights())
+        assert cam is None
+
+
+def test_scene_desc_files_match_the_benchmark_scenes():
+    objs, mats, lts, cam = rt.parse_scene(open(os.path.join(ROOT, "scenes", "config1.json")).read())
+    assert as_bytes(objs) == as_bytes(scenes.config1_objects())
+    objs, _, _, _ = rt.parse_scene(open(os.path.join(ROOT, "scenes", "config2.json")).read())
+    assert as_bytes(objs) == as_bytes(scenes.bench_objects(16))
+
+
+def test_scene_desc_explicit_tables_and_camera():
+    text = """{
+      "materials": [{"name": "gold", "ambient": [0.25, 0.2, 0.07], "diffuse": [0.75, 0.6, 0.23, 0.5],
+                     "specular": [0.63, 0.56, 0.37], "shininess": 51.2},
+                    {"name": "glass", "transparency": 0.9, "refraction_index": 1.5}],
+      "lights": [{"position": [1, 2, 3], "ambient": [0.1, 0.1, 0.1], "diffuse": [1, 1, 1], "specular": [1, 1, 1]}],
+      "objects": [{"sphere": {"position": [0, 0, 1], "radius": 2}, "material": "gold"},
+                  {"box": {"mins": [-1, -1, -1], "maxs": [1, 1, 1], "position": [0, 3, 0], "angles": [10, 20, 30]},
+                   "material": 1}],
+      "camera": {"position": [5, 0, 1], "angles": [0, 180, 0], "v_fov": 60}
+    }"""
+    objs, mats, lts, cam = rt.parse_scene(text)
+    assert len(mats) == 2 and len(lts) == 1 and len(objs) == 2
+    assert list(mats[0].diffuse) == pytest.approx([0.75, 0.6, 0.23, 0.5])
+    assert list(mats[0].ambient) == pytest.approx([0.25, 0.2, 0.07, 1.0])  # 3 components: alpha 1
+    assert mats[1].refraction_index == 1.5 and mats[1].transparency == pytest.approx(0.9)
+    assert mats[0].refraction_index == 1.0  # default
+    assert objs[0].radius == 2.0 and objs[0].material == 0 and list(objs[0].box_maxs) == [0, 0, 0]
+    assert objs[1].radius == -1.0 and objs[1].material == 1 and list(objs[1].angles) == [10, 20, 30]
+    assert list(cam.position) == [5, 0, 1] and cam.v_fov == 60
+    ref = rt.reference_camera(0.0)
+    assert cam.near_plane == ref.near_plane and cam.aspect == ref.aspect  # unset lens fields: the reference's
+
+
+@pytest.mark.parametrize("text,fragment", [
+    ('{"objects": [1,]}', "offset"),
+    ('{"objects": [{"sphere": {"radius": 1}, "material": "nope"}]}', "unknown material"),
+    ('{"objects": [{"sphere": {"radius": 1}, "material": 7}]}', "out of range"),
+    ('{"objects": [{"sphere": {"radius": 1}}]}', "needs a material"),
+    ('{"objects": [{"bench_spheres": {"count": 5000}}]}', "too many"),
+    ('{"lights": [{"position": [1, 2]}]}', "expected 3 numbers"),
+    ('[1, 2]', "JSON object"),
+    ('{"objects": "reference"} x', "trailing"),
+])
+def test_scene_desc_errors_are_reported(text, fragment):
+    with pytest.raises(rt.RTError) as e:
+        rt.parse_scene(text)
+    assert e.value.code == rt.abi.RT_ERR_INVALID and fragment in str(e.value)
