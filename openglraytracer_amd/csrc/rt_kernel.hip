@@ -191,6 +191,19 @@ struct Ray {
     v3 start, dir;
 };
 
+// A record read through the constant address space, dword by dword (scalar
+// loads when the address is wave-uniform).
+template <class T>
+__device__ __forceinline__ T cload(const __attribute__((address_space(4))) T *p) {
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    T r;
+    const __attribute__((address_space(4))) uint32_t *src = (const __attribute__((address_space(4))) uint32_t *)p;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&r);
+#pragma unroll
+    for (int i = 0; i < static_cast<int>(sizeof(T) / 4); ++i) dst[i] = src[i];
+    return r;
+}
+
 // LDS-resident scene view.
 struct Scene {
     const float4 *sph;      // cx, cy, cz, r*r
@@ -204,6 +217,11 @@ struct Scene {
     const LightMatRec *lm;
     const float4 *bvh;  // BvhNode pairs (lo, hi)
     const ShadowCone *cone;  // [light][sphere] shadow culling cones
+    // The same box and light records in the device blob through the constant
+    // address space: a wave-uniform record index becomes scalar loads into
+    // SGPRs (no LDS round trip, no VGPRs) — used where the index is uniform.
+    const __attribute__((address_space(4))) BoxRec *cbox;
+    const __attribute__((address_space(4))) LightRec *clight;
     int ns, nb, nl, nm, nbvh;
     int cull;
     int tx0, tx1, ty0, ty1;  // this wave's pixel rectangle (frame coordinates)
@@ -386,7 +404,7 @@ template <bool kPrimary>
 __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
     Hit h{10000.0f, -1, 0, false, mk(0.0f, 0.0f, 0.0f)};
     for (int b = 0; b < S.nb; ++b) {
-        const BoxRec &B = S.box[b];
+        const BoxRec B = cload(S.cbox + b);
         v3 rs;
         bool inside;
         if (kPrimary) {
@@ -432,7 +450,8 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
             if (node_hit(q, lo, hi, h.t)) {
                 if (leaf) {
                     const int first = leaf & 0xFFFFFF, count = leaf >> 24;
-                    for (int s = first; s < first + count; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, false, h);
+                    for (int s = first; s < first + count; ++s)
+                        test_sphere(S, s, r.start, d2, qa2, qa4, false, h);
                     node = __float_as_int(lo.w);
                 } else {
                     node = node + 1;
@@ -455,7 +474,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     for (int b = 0; b < S.nb; ++b)
-        if (need && !hit) hit = box_occludes(S.box[b], start, dir, light_bit);
+        if (need && !hit) hit = box_occludes(cload(S.cbox + b), start, dir, light_bit);
     if (!__any(need && !hit)) return hit;
     const v3 d2 = muls(dir, 2.0f);
     const float qa = dot(dir, dir);
@@ -631,8 +650,9 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
     float4 dif = make_float4(0.0f, 0.0f, 0.0f, 0.0f), spe = dif;
     const v3 view = normalize(muls(r.dir, -1.0f));
     for (int j = 0; j < S.nl; ++j) {
-        if (S.light[j].dead != 0.0f) continue;  // no direct term for any material (host-checked)
-        const v3 lpos = mk(S.light[j].pos[0], S.light[j].pos[1], S.light[j].pos[2]);
+        const LightRec L = cload(S.clight + j);
+        if (L.dead != 0.0f) continue;  // no direct term for any material (host-checked)
+        const v3 lpos = mk(L.pos[0], L.pos[1], L.pos[2]);
         const v3 ldir = normalize(sub(lpos, c.p));
         const v3 lref = normalize(reflect(muls(ldir, -1.0f), c.n));
         const float cos_theta = dot(ldir, c.n);
@@ -1074,6 +1094,8 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
     S.bvh = lds + p.off_bvh;
     S.cone = p.off_cone >= 0 ? reinterpret_cast<const ShadowCone *>(lds + p.off_cone) : nullptr;
+    S.cbox = (const __attribute__((address_space(4))) BoxRec *)(static_cast<const float4 *>(p.scene) + p.off_boxes);
+    S.clight = (const __attribute__((address_space(4))) LightRec *)(static_cast<const float4 *>(p.scene) + p.off_lights);
     S.nbvh = p.n_bvh;
     S.ns = p.n_spheres;
     S.nb = p.n_boxes;
