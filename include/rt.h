@@ -201,6 +201,16 @@ int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views
                     int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
                     void *hip_stream);
 
+/* Animated frames in one launch (the reference's frame loop, main.cpp:81-86,
+ * where the shipped scene moves with `time`, raytrace_compute.glsl:277-307):
+ * as rt_render_batch, but views[k] renders scenes[k]. Every scene must have
+ * scene 0's layout — the same object kinds in the same order and the same
+ * material and light counts (e.g. rt_reference_objects at successive times,
+ * each built with rt_scene_create). */
+int rt_render_batch_scenes(rt_context *ctx, const rt_scene *const *scenes, const rt_view *views, int n_views,
+                           int width, int height, int max_depth, int block_rows, int n_shards, int shard,
+                           float *out_device, void *hip_stream);
+
 /* Monte-Carlo extension (the reference has one
  * ray per pixel): adds, for every pixel of rows [row_begin, row_end), the sum
  * of samples [sample_offset, sample_offset + spp) — in sample order — to

@@ -67,6 +67,7 @@ def lib():
             "rt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i),
             "rt_context_set": ([vp, i, i], i),
             "rt_render_batch": ([vp, vp, vp, i, i, i, i, i, i, i, vp, vp], i),
+            "rt_render_batch_scenes": ([vp, vp, vp, i, i, i, i, i, i, i, vp, vp], i),
             "rt_render_accumulate": ([vp, vp, vp, i, i, i, i, i, C.c_uint32, i, i, i, vp, vp], i),
             "rt_pack_rgba8": ([vp, C.c_size_t, vp], i),
             "rt_write_ppm": ([C.c_char_p, vp, i, i], i), "rt_write_pfm": ([C.c_char_p, vp, i, i], i),
@@ -313,6 +314,16 @@ def render_batch(ctx, scene, out_ptr, width, height, max_depth, views, block_row
     _check(lib().rt_render_batch(ctx.handle, scene.handle, arr, len(views), width, height, max_depth,
                                  block_rows, n_shards, shard, C.c_void_p(out_ptr),
                                  C.c_void_p(stream) if stream else None))
+
+
+def render_batch_scenes(ctx, scenes, out_ptr, width, height, max_depth, views, block_rows=8, n_shards=1,
+                        shard=0, stream=None):
+    """K animated frames in one launch: views[k] of scenes[k] (same layout),
+    into device memory (K, rows, width, 4)."""
+    arr = (View * len(views))(*views)
+    sarr = (C.c_void_p * len(scenes))(*[s.handle for s in scenes])
+    _check(lib().rt_render_batch_scenes(ctx.handle, sarr, arr, len(views), width, height, max_depth, block_rows,
+                                        n_shards, shard, C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None))
 
 
 def render_accumulate(ctx, scene, accum_ptr, width, height, max_depth, spp, sample_offset=0, seed=0,

@@ -346,9 +346,23 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
     return RT_OK;
 }
 
-int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views, int width,
-                    int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
-                    void *hip_stream) {
+}  // extern "C"
+
+namespace {
+// Same blob layout (section offsets and counts): views of these scenes can
+// share one launch, each work-group staging its own view's blob.
+bool same_layout(const DeviceScene &a, const DeviceScene &b) {
+    return a.blob_units == b.blob_units && a.off_spheres == b.off_spheres && a.off_smeta == b.off_smeta &&
+           a.off_boxes == b.off_boxes && a.off_mats == b.off_mats && a.off_lights == b.off_lights &&
+           a.off_lightmat == b.off_lightmat && a.off_bvh == b.off_bvh && a.n_bvh == b.n_bvh &&
+           a.off_cone == b.off_cone && a.n_spheres == b.n_spheres && a.n_boxes == b.n_boxes &&
+           a.n_mats == b.n_mats && a.n_lights == b.n_lights;
+}
+
+int render_batch_impl(rt_context *ctx, const rt_scene *const *scenes, const rt_view *views, int n_views, int width,
+                      int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
+                      void *hip_stream) {
+    const rt_scene *scene = scenes[0];
     int rc = check_render_args(ctx, scene, width, height, max_depth);
     if (rc != RT_OK) return rc;
     if (!views || n_views <= 0 || n_views > RT_MAX_BATCH || !out_device) {
@@ -365,6 +379,15 @@ int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail("hipSetDevice", e);
     LaunchParams p = base_params(ctx, scene, views, n_views, width, height);
+    for (int k = 1; k < n_views; ++k) {
+        if (scenes[k] == scene) continue;
+        if (!scenes[k] || scenes[k]->device != ctx->device || !same_layout(scenes[k]->dev, scene->dev)) {
+            set_error("rt_render_batch_scenes: scene " + std::to_string(k) +
+                      " is missing, on another device or laid out differently from scene 0");
+            return RT_ERR_INVALID;
+        }
+        p.view[k].blob = scenes[k]->dev.blob;
+    }
     p.row_begin = 0;
     p.n_rows = rows;
     if (sharded) {
@@ -381,6 +404,30 @@ int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views
         if (e != hipSuccess) return hip_fail("render", e);
     }
     return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views, int width,
+                    int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
+                    void *hip_stream) {
+    const rt_scene *scenes[RT_MAX_BATCH];
+    for (int k = 0; k < RT_MAX_BATCH; ++k) scenes[k] = scene;
+    return render_batch_impl(ctx, scenes, views, n_views, width, height, max_depth, block_rows, n_shards, shard,
+                             out_device, hip_stream);
+}
+
+int rt_render_batch_scenes(rt_context *ctx, const rt_scene *const *scenes, const rt_view *views, int n_views,
+                           int width, int height, int max_depth, int block_rows, int n_shards, int shard,
+                           float *out_device, void *hip_stream) {
+    if (!scenes || !scenes[0]) {
+        set_error("rt_render_batch_scenes: null scenes");
+        return RT_ERR_INVALID;
+    }
+    return render_batch_impl(ctx, scenes, views, n_views, width, height, max_depth, block_rows, n_shards, shard,
+                             out_device, hip_stream);
 }
 
 int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width, int height,

@@ -101,6 +101,7 @@ struct FrameView {
     float proj[16];    // column-major proj*view = inverse(unproj) (float64 on the host), for culling
     float origin[3];   // ray start = camera position (:391)
     int32_t cull;      // 1: exactness-preserving culling enabled (consistent pinhole view)
+    const void *blob;  // this view's scene blob (rt_render_batch_scenes); nullptr: LaunchParams::scene
 };
 constexpr int kMaxViews = 8;  // frames per launch (blockIdx.z)
 

@@ -831,6 +831,15 @@ __device__ __forceinline__ uint32_t unorm8(float v) {
     return static_cast<uint32_t>(v * 255.0f + 0.5f);
 }
 
+// One pixel's colour into the launch's surface (float4 or GL_RGBA8 bytes).
+__device__ __forceinline__ void store_pixel(const LaunchParams &p, int z, size_t idx, v3 col) {
+    const size_t at = static_cast<size_t>(z) * p.n_rows * p.width + idx;
+    if (p.out_rgba8)  // GL_RGBA8 unorm store of vec4(rgb, 0.0) (main.cpp:223, :404): rt_pack_rgba8
+        reinterpret_cast<uint32_t *>(p.out)[at] = unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16);
+    else
+        p.out[at] = make_float4(col.x, col.y, col.z, 0.0f);
+}
+
 // Counter-based sample jitter (Monte-Carlo extension):
 // a 32-bit integer hash of (seed, sample, pixel, axis); u in [0, 1) with 24
 // bits. Integer-only, so the oracle reproduces it exactly.
@@ -878,7 +887,7 @@ __device__ __forceinline__ float group8_max(float v) {
 // bounding cube each (group-of-8 DPP min / max), to keep the prologue short.
 __device__ __forceinline__ void frame_setup(const LaunchParams &p, const FrameView &V, float4 *sph_cam,
                                             int4 *sph_px, float4 *box_cam) {
-    const float4 *blob = static_cast<const float4 *>(p.scene);
+    const float4 *blob = static_cast<const float4 *>(V.blob ? V.blob : p.scene);
     const v3 origin = mk(V.origin[0], V.origin[1], V.origin[2]);
     const int hw = p.width / 2, hh = p.height / 2;
     const bool cull = V.cull && hw > 0 && hh > 0;
@@ -1003,16 +1012,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         if constexpr (kDepth == 0) col = trace0(S, ray, active);
         else col = trace_tree<kDepth>(S, ray, active);
 #endif
-        if (active) {
-            if (p.out_rgba8) {
-                // GL_RGBA8 unorm store of vec4(rgb, 0.0) (main.cpp:223, :404):
-                // clamp (NaN -> 0), v * 255 + 0.5, truncate — rt_pack_rgba8
-                reinterpret_cast<uint32_t *>(p.out)[static_cast<size_t>(z) * p.n_rows * p.width + idx] =
-                    unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16);
-            } else {
-                out[idx] = make_float4(col.x, col.y, col.z, 0.0f);
-            }
-        }
+        if (active) store_pixel(p, z, idx, col);
     } else {
         const uint32_t pixel = static_cast<uint32_t>(y) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x);
         v3 acc = mk(0.0f, 0.0f, 0.0f);
@@ -1066,7 +1066,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // ---- prologue: stage the scene blob into LDS and derive the view's
     // per-frame constants (both from the device blob, one barrier); the tiled
     // path computes its camera rays while the staging loads are in flight ----
-    const float4 *blob = static_cast<const float4 *>(p.scene);
+    const float4 *blob = static_cast<const float4 *>(V.blob ? V.blob : p.scene);
     const int tid = threadIdx.x;
     float4 first = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (tid < p.blob_units) first = blob[tid];
@@ -1094,8 +1094,8 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
     S.bvh = lds + p.off_bvh;
     S.cone = p.off_cone >= 0 ? reinterpret_cast<const ShadowCone *>(lds + p.off_cone) : nullptr;
-    S.cbox = (const __attribute__((address_space(4))) BoxRec *)(static_cast<const float4 *>(p.scene) + p.off_boxes);
-    S.clight = (const __attribute__((address_space(4))) LightRec *)(static_cast<const float4 *>(p.scene) + p.off_lights);
+    S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
+    S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
     S.nbvh = p.n_bvh;
     S.ns = p.n_spheres;
     S.nb = p.n_boxes;

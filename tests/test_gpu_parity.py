@@ -414,3 +414,26 @@ def test_cli_renders_a_scene_description(gpu_ctx, tmp_path):
     assert data.startswith(header)
     img = np.frombuffer(data[len(header):], np.uint8).reshape(48, 64, 3)
     assert np.array_equal(img, rt.pack_rgba8(f)[::-1, :, :3])  # PPM rows top-down
+
+
+def test_animated_frames_in_one_launch(gpu_ctx):
+    """rt_render_batch_scenes: K frames of the shipped, time-animated scene
+    (raytrace_compute.glsl:277-307, the camera orbiting, main.cpp:81-86) in
+    one launch, each frame its own scene — equal to K single renders and to
+    the oracle; a scene of another layout is refused."""
+    times = [0.0, 0.25, 1.5, 4.0]
+    w, h, depth = 96, 54, 2
+    scs = [rt.Scene(gpu_ctx, rt.reference_objects(t)) for t in times]
+    views = [rt.make_view(None, t) for t in times]
+    out = torch.zeros((len(times), h, w, 4), dtype=torch.float32, device="cuda")
+    rt.render_batch_scenes(gpu_ctx, scs, out.data_ptr(), w, h, depth, views)
+    got = out.cpu().numpy()
+    for k, t in enumerate(times):
+        assert np.array_equal(got[k], rt.render(gpu_ctx, scs[k], w, h, depth, view=views[k])), k
+        assert np.array_equal(got[k], oracle_render(rt.reference_objects(t), w, h, depth, t)), k
+    other = rt.Scene(gpu_ctx, scenes.bench_objects(4))
+    with pytest.raises(rt.RTError) as e:
+        rt.render_batch_scenes(gpu_ctx, [scs[0], other], out.data_ptr(), w, h, depth, views[:2])
+    assert e.value.code == rt.abi.RT_ERR_INVALID
+    for s in scs + [other]:
+        s.close()
