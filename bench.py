@@ -82,18 +82,32 @@ def cpu_baseline(budget_s):
     return None
 
 
-def pmc_traffic(workload):
-    """Per-launch HBM bytes of the render kernel from the committed PMC pass
-    (profiles/pmc_latest.json, written by tools/pmc_summary.py), or None."""
+def pmc_latest(workload):
+    """The committed PMC summary of the render kernel (profiles/pmc_latest.json,
+    written by tools/pmc_summary.py) for this workload at N=1, or {}."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
         if d.get("workload") == workload and d.get("n_gpus", 1) == 1:
-            return d.get("hbm_bytes_per_launch")
+            return d
     except (OSError, ValueError):
         pass
-    return None
+    return {}
+
+
+def valu_bound(pmc, kernel_ms):
+    """The bound the kernel actually sits against: VALU issue.
+    Peak = one wave64 VALU instruction per 2 cycles per SIMD (SIMD-32),
+    1024 SIMDs at 2.4 GHz (/opt/skills/guides/MI355X_MICROARCH.md)."""
+    insts = pmc.get("sq_insts_valu_per_launch")
+    if not insts or kernel_ms <= 0:
+        return None
+    peak = 1024 * 2.4e9 / 2 / 1e12  # T wave-instructions / s
+    achieved = insts / (kernel_ms * 1e-3) / 1e12
+    return {"wave_insts_per_launch": insts, "achieved": round(achieved, 4), "peak": round(peak, 4),
+            "unit": "T wave-instr/s", "frac": round(achieved / peak, 4),
+            "source": "SQ_INSTS_VALU from profiles/pmc_latest.json (same build's rocprofv3 --pmc pass)"}
 
 
 def main():
@@ -238,7 +252,8 @@ def main():
     value = rays_per_step * args.steps / elapsed / 1e6
     avg_kernel_ms = float(np.mean(kernel_ms))
     achieved = px_per_launch * BYTES_PER_PIXEL / (avg_kernel_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args.workload) if world == 1 else None
+    pmc = pmc_latest(args.workload) if world == 1 else {}
+    traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not mc:
@@ -274,7 +289,8 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_ms, 5),
-                         "bytes_per_launch": px_per_launch * BYTES_PER_PIXEL},
+                         "bytes_per_launch": px_per_launch * BYTES_PER_PIXEL,
+                         "valu": valu_bound(pmc, avg_kernel_ms)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
