@@ -90,6 +90,7 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.out_rgba8 = ctx->output == RT_OUTPUT_RGBA8 ? 1 : 0;
     p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
+    host_frame_setup(p, scene->host.empty() ? nullptr : scene->host.data());
     return p;
 }
 
@@ -198,6 +199,7 @@ int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt
     }
     s->device = ctx->device;
     s->dev = ds;
+    s->host.swap(blob);
     s->capacity_units = ds.blob_units > 0 ? ds.blob_units : 1;
     *out = s;
     return RT_OK;
@@ -241,6 +243,7 @@ int rt_scene_update(rt_context *ctx, rt_scene *scene, const rt_object *objs, int
     void *keep = scene->dev.blob;
     scene->dev = ds;
     scene->dev.blob = keep;
+    scene->host.swap(blob);
     return RT_OK;
 }
 

@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/rt.h"
 
@@ -104,6 +105,7 @@ struct FrameView {
     const void *blob;  // this view's scene blob (rt_render_batch_scenes); nullptr: LaunchParams::scene
 };
 constexpr int kMaxViews = 8;  // frames per launch (blockIdx.z)
+constexpr int kMaxFrameConsts = 144;  // 2 x spheres + boxes carried in the kernel arguments (64 spheres + 16 boxes)
 
 struct LaunchParams {
     FrameView view[kMaxViews];
@@ -131,7 +133,14 @@ struct LaunchParams {
     int32_t *sched;
     int32_t n_cu;
     int32_t out_rgba8;  // 1: store GL_RGBA8 unorm bytes (uchar4 per pixel) instead of float4
+    // The view's per-frame constants ([sphere camera terms][sphere pixel
+    // footprints][box camera terms], the LDS image the kernel's frame_setup
+    // derives), computed on the host when a one-view launch's fit here
+    // (host_frame_setup); 0: every work-group derives them.
+    int32_t n_frame_consts;
+    float4 frame_consts[kMaxFrameConsts];
 };
+static_assert(sizeof(LaunchParams) <= 4096, "kernel arguments must stay within 4 KiB");
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
 constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
 constexpr int kSchedInts = 2 * kQueues * kQueueStride; // heads + done counters of one launch
@@ -144,6 +153,13 @@ struct DeviceScene {
     int32_t off_bvh = 0, n_bvh = 0, off_cone = 0;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
+
+// rt_scene.cpp: the view's per-frame constants on the host, bit-identical to
+// the kernel's frame_setup for the camera terms (float32, same operation
+// order) and conservative pixel footprints; writes 2 * n_spheres + n_boxes
+// records into p.frame_consts and sets p.n_frame_consts, or leaves 0 when
+// they do not fit.
+void host_frame_setup(LaunchParams &p, const float4 *blob);
 
 // rt_kernel.hip
 hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t stream);
@@ -172,5 +188,6 @@ struct rt_context {
 struct rt_scene {
     int device = 0;
     rtamd::DeviceScene dev;
+    std::vector<float4> host;    // host copy of the blob (per-frame constants on the host)
     int32_t capacity_units = 0;  // allocated blob size (16-B units)
 };

@@ -48,10 +48,15 @@ namespace {
 #ifndef RT_WAVES_Y
 #define RT_WAVES_Y 2
 #endif
+#ifndef RT_TILE_ROUNDS
+#define RT_TILE_ROUNDS 1
+#endif
 // A work-group renders a tile of kWavesX x kWavesY wave footprints of 8x8 pixels.
 constexpr int kWavesX = RT_WAVES_X, kWavesY = RT_WAVES_Y;
 constexpr int kTileX = 8 * kWavesX, kTileY = 8 * kWavesY;
 constexpr int kThreads = 64 * kWavesX * kWavesY;
+// tiled distribution: a work-group renders kRounds tiles, strided down the frame
+constexpr int kRounds = RT_TILE_ROUNDS;
 
 struct v3 {
     float x, y, z;
@@ -644,6 +649,24 @@ __device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const
     return c;
 }
 
+// Development probe (timing builds only, tools/phase_trace.py): lane 0 of
+// every wave of a depth-0 tiled launch records the 100 MHz real-time clock
+// at fixed points of its life.
+#ifdef RT_PHASE_TRACE
+constexpr unsigned kPhaseWaves = 1u << 17;
+__device__ unsigned long long rt_phase_buf[kPhaseWaves * 16];
+#define RT_PHASE(k)                                                                                        \
+    do {                                                                                                    \
+        const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();                                   \
+        const unsigned wg_ = (blockIdx.y * gridDim.x + blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); \
+        if ((threadIdx.x & 63) == 0 && wg_ < kPhaseWaves) rt_phase_buf[wg_ * 16 + (k)] = now_;              \
+    } while (0)
+#else
+#define RT_PHASE(k) \
+    do {            \
+    } while (0)
+#endif
+
 // ads_phong_lighting (:789-840). Called with all lanes active.
 __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collision &c, bool valid) {
     const MatRec &m = S.mat[c.material];
@@ -674,6 +697,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         // zero product adds +-0 to sums that are never -0)
         const bool changes = q.always || (kd != 0.0f && q.d_nz) || (ks != 0.0f && q.s_nz);
         const bool need = valid && changes;
+        if (j == 1) RT_PHASE(5);
 #ifdef RT_ABLATE_SHADOW
         if (need) { dif = nd; spe = ns; }
         continue;
@@ -686,6 +710,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
             }
         }
     }
+    RT_PHASE(6);
     // phong = ambient + diffuse + specular + emissive; return rgb * a (:837-839)
     const float px = ((m.amb_sum[0] + dif.x) + spe.x) + m.emissive[0];
     const float py = ((m.amb_sum[1] + dif.y) + spe.y) + m.emissive[1];
@@ -708,10 +733,13 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
 // with valid = false.
 __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
+    RT_PHASE(2);
     const Hit h = closest<true>(S, r, valid);
+    RT_PHASE(3);
     const bool hit = valid && h.obj >= 0;
     if (!__any(hit)) return black;  // per-wave early out
     const Collision c = resolve<true>(S, r, h, hit);
+    RT_PHASE(4);
 #ifdef RT_ABLATE_PHONG
     const v3 col = add(c.p, c.n);
 #else
@@ -863,7 +891,10 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 // waves per SIMD (config 4: 58 -> 37 ms; config 3: 1.52 -> 1.37 ms); depth 0/1
 // need fewer registers than that anyway.
 #ifndef RT_WAVES_PER_EU
-#define RT_WAVES_PER_EU(d) ((d) >= 2 ? 6 : 1)
+#ifndef RT_WPE0
+#define RT_WPE0 1
+#endif
+#define RT_WAVES_PER_EU(d) ((d) >= 2 ? 6 : ((d) == 0 ? RT_WPE0 : 1))
 #endif
 #define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(kDepth))))
 // Reductions over aligned groups of 8 lanes (DPP: quad butterflies, then the
@@ -1066,10 +1097,25 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // ---- prologue: stage the scene blob into LDS and derive the view's
     // per-frame constants (both from the device blob, one barrier); the tiled
     // path computes its camera rays while the staging loads are in flight ----
+    RT_PHASE(0);
+#ifdef RT_PHASE_TRACE
+    {  // where the wave runs: HW_ID (cu / simd / se) and XCC_ID
+        const unsigned wg_ = (blockIdx.y * gridDim.x + blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6);
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        if ((threadIdx.x & 63) == 0 && wg_ < kPhaseWaves) {
+            rt_phase_buf[wg_ * 16 + 8] = hw;
+            rt_phase_buf[wg_ * 16 + 9] = xcc;
+        }
+    }
+#endif
     const float4 *blob = static_cast<const float4 *>(V.blob ? V.blob : p.scene);
     const int tid = threadIdx.x;
-    float4 first = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 first = make_float4(0.0f, 0.0f, 0.0f, 0.0f), fc = first;
     if (tid < p.blob_units) first = blob[tid];
+    // per-frame constants computed on the host (one-view launches, small
+    // scenes: host_frame_setup) — else derived below by every work-group
+    static_assert(kMaxFrameConsts <= kThreads, "one record per thread");
+    if (tid < p.n_frame_consts) fc = p.frame_consts[tid];
     float4 *sph_cam = lds + p.blob_units;
     int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
     float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
@@ -1078,10 +1124,18 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     const Pixel own = wave_pixel(p, own_wx, own_wy);
     Ray own_ray;
     if (!queued && !kAccum) own_ray = camera_ray(p, V, own.x, own.y, 0.0f, 0.0f);
+    RT_PHASE(10);
     if (tid < p.blob_units) lds[tid] = first;
+    RT_PHASE(11);
     for (int i = tid + kThreads; i < p.blob_units; i += kThreads) lds[i] = blob[i];
-    frame_setup(p, V, sph_cam, sph_px, box_cam);
+    if (p.n_frame_consts > 0) {
+        if (tid < p.n_frame_consts) sph_cam[tid] = fc;
+    } else {
+        frame_setup(p, V, sph_cam, sph_px, box_cam);
+    }
+    RT_PHASE(12);
     __syncthreads();
+    RT_PHASE(13);
     Scene S;
     S.sph = lds + p.off_spheres;
     S.smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
@@ -1113,6 +1167,22 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // of queue q (its first q_waves items are dealt statically), then the
     // queue's head (one render call site for both: the kernel body is inlined once)
     int t = queued ? g : 0;
+    RT_PHASE(1);
+#if RT_TILE_ROUNDS > 1
+    if (!queued) {
+        const int stride_y = static_cast<int>(gridDim.y) * kWavesY;
+        if constexpr (!kAccum)
+            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, &own_ray);
+        else
+            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, nullptr);
+        for (int r = 1; r < kRounds; ++r) {
+            const int wy = own_wy + r * stride_y;
+            if (wy * 8 >= p.n_rows) break;
+            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, wy, z, wave_pixel(p, own_wx, wy), nullptr);
+        }
+        return;
+    }
+#endif
     while (t < total) {
         int nxt = 0;
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
@@ -1121,6 +1191,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
                                          (queued || kAccum) ? nullptr : &own_ray);
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
+    RT_PHASE(7);
     if (!queued) return;
     if (lane == 0 && atomicAdd(done, 1) == q_waves - 1) {
         atomicExch(head, 0);  // every wave of the queue has made its last fetch
@@ -1154,7 +1225,7 @@ template <int kDepth, bool kAccum>
 hipError_t launch_kernel(LaunchParams p, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
     const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
-    dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY - 1) / kTileY, p.n_views);
+    dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY * kRounds - 1) / (kTileY * kRounds), p.n_views);
     const int wave_tiles = ((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
     if (kQueuedDepth(kDepth) && p.sched && p.n_views == 1 && wave_tiles > resident * (kThreads / 64)) {
@@ -1210,3 +1281,22 @@ hipError_t allow_large_lds(size_t bytes) {
 }
 
 }  // namespace rtamd
+
+#ifdef RT_PHASE_TRACE
+extern "C" int rt_debug_phase_read(void *dst, size_t bytes) {
+    const size_t n = bytes < sizeof(rtamd::rt_phase_buf) ? bytes : sizeof(rtamd::rt_phase_buf);
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(rtamd::rt_phase_buf), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int rt_debug_occupancy(size_t lds) {
+    int n = -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&rtamd::render_kernel<0, false>),
+                                                     rtamd::kThreads, lds) != hipSuccess)
+        return -1;
+    return n;
+}
+extern "C" int rt_debug_phase_clear(void) {
+    void *ptr = nullptr;
+    if (hipGetSymbolAddress(&ptr, HIP_SYMBOL(rtamd::rt_phase_buf)) != hipSuccess) return -1;
+    return hipMemset(ptr, 0, sizeof(rtamd::rt_phase_buf)) == hipSuccess ? 0 : -1;
+}
+#endif

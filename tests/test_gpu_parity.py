@@ -146,6 +146,47 @@ def test_batched_frames_equal_single_frames(gpu_ctx, n_shards):
     sc.close()
 
 
+def _inside_sphere_camera():
+    cam = rt.Camera()
+    cam.position[:] = (-3.0, 4.0, 1.2)  # inside config 1's red-glass sphere (centre (-3, 4, 1), r 2)
+    cam.angles[:] = (0.3, 1.1, 0.0)
+    cam.v_fov, cam.aspect, cam.near_plane, cam.far_plane = 1.5707964, 16.0 / 9.0, 0.1, 1000.0
+    return cam
+
+
+@pytest.mark.parametrize("case", ["bench16", "bench64", "shipped", "inside_sphere", "no_culling"])
+def test_host_frame_constants_equal_device_ones(gpu_ctx, case):
+    """A one-view launch takes its per-frame constants from the host
+    (host_frame_setup, carried in the kernel arguments); a batch launch
+    derives them in every work-group (frame_setup). Both must give the same
+    frame, bit for bit — camera terms identical, footprints conservative."""
+    w, h, depth, cam = 256, 144, 1, None
+    if case in ("bench16", "no_culling"):
+        objs, view_t = scenes.bench_objects(16), 0.4
+    elif case == "bench64":
+        objs, view_t, depth = scenes.bench_objects(64), 2.0, 2
+    elif case == "shipped":
+        objs, view_t = rt.reference_objects(1.3), 1.3
+    else:
+        objs, view_t, cam = scenes.config1_objects(), 0.0, _inside_sphere_camera()
+    view = rt.make_view(cam, view_t)
+    if case == "no_culling":
+        gpu_ctx.set_culling(False)
+    try:
+        sc = rt.Scene(gpu_ctx, objs)
+        single = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+        out = torch.zeros((2, h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, [view, view])
+        got = out.cpu().numpy()
+        sc.close()
+    finally:
+        gpu_ctx.set_culling(True)
+    assert np.array_equal(got[0], single) and np.array_equal(got[1], single)
+    if case in ("bench16", "shipped"):
+        o = oracle_render(objs, w, h, depth, view_t)
+        assert np.array_equal(single, o), parity_stats(single, o)
+
+
 def test_async_stream_equals_sync(gpu_ctx):
     objs = scenes.bench_objects(16)
     view = rt.make_view(None, 1.0)
