@@ -340,20 +340,58 @@ __device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, 
 }
 
 // ---- spheres (:583-640) --------------------------------------------------
+// The shader divides both roots' numerators n1 = -qb + sq >= n2 = -qb - sq by
+// qa2 and then picks one by the quotients' signs. For qa2 a normal float in
+// [2^-100, 2^100] and |n1|, |n2| >= qa2 * 2^-100 (`floor`, per ray) neither
+// quotient underflows, so each has its numerator's sign, t1 >= t2 (correctly
+// rounded division is monotonic), and the choice can be made on the
+// numerators: one division instead of two, bit-identical. Otherwise (zero or
+// tiny numerators, qa2 zero or huge; floor = NaN) the shader's arithmetic runs
+// as written. NaN numerators pass the check only towards a NaN or a -1 result,
+// both misses, as in the shader.
+__device__ __forceinline__ float root_floor(float qa2) {
+    return (qa2 >= 0x1p-100f && qa2 <= 0x1p100f) ? qa2 * 0x1p-100f : __builtin_nanf("");
+}
 // intersect_sphere_object's t (:586-625) from the ray-invariant terms.
-__device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float qa4, bool &inside) {
+__device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float qa4, float floor, bool &inside) {
     const float qd = qb * qb - qa4 * qc;
     if (qd < 0.0f) return -1.0f;
     const float sq = sqrtf(qd);
-    const float t1 = (-qb + sq) / qa2;
-    const float t2 = (-qb - sq) / qa2;
+    const float n1 = -qb + sq, n2 = -qb - sq;
+#ifndef RT_TWO_DIV
+    if (fminf(fabsf(n1), fabsf(n2)) >= floor) {
+        if (n1 < 0.0f) return -1.0f;  // t_far < 0
+        inside = n2 < 0.0f;           // t_near < 0
+        return (inside ? n1 : n2) / qa2;
+    }
+#endif
+    const float t1 = n1 / qa2;
+    const float t2 = n2 / qa2;
     const float tn = gmin(t1, t2), tf = gmax(t1, t2);
     if (tf < 0.0f) return -1.0f;
     inside = tn < 0.0f;
     return inside ? tf : tn;
 }
+// Shadow test of one sphere: sphere_t's t in (0, 1), deciding fl(n / qa2) < 1
+// without the division unless n is within 2^-16 of qa2 (quotient_below_one).
+__device__ __forceinline__ bool sphere_blocks(float qb, float qc, float qa2, float qa4, float floor) {
+    const float qd = qb * qb - qa4 * qc;
+    if (!(qd >= 0.0f)) return false;
+#ifndef RT_TWO_DIV
+    const float sq = sqrtf(qd);
+    const float n1 = -qb + sq, n2 = -qb - sq;
+    if (fminf(fabsf(n1), fabsf(n2)) >= floor) {
+        if (n1 < 0.0f) return false;
+        const float n = n2 < 0.0f ? n1 : n2;
+        return n > 0.0f && quotient_below_one(n, qa2);
+    }
+#endif
+    bool inside;
+    const float t = sphere_t(qb, qc, qa2, qa4, __builtin_nanf(""), inside);
+    return t > 0.0f && t < 1.0f;
+}
 
-__device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 d2, float qa2, float qa4,
+__device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 d2, float qa2, float qa4, float floor,
                                             bool primary, Hit &h) {
     float qb, qc;
     if (primary) {
@@ -369,7 +407,7 @@ __device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 
     const float qd = qb * qb - qa4 * qc;
     if (qd >= 0.0f) {  // rare per sphere: keep the divisions off the common path
         bool inside = false;
-        const float t = sphere_t(qb, qc, qa2, qa4, inside);
+        const float t = sphere_t(qb, qc, qa2, qa4, floor, inside);
         const int obj = S.smeta[s].x;
         if (closer(t, obj, h)) {
             h.t = t;
@@ -428,6 +466,7 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
     const v3 d2 = muls(r.dir, 2.0f);
     const float qa = dot(r.dir, r.dir);
     const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
+    const float floor = root_floor(qa2);
     if (kPrimary && S.cull) {
         // spheres whose conservative footprint overlaps this wave's tile
         const int lane = threadIdx.x & 63;
@@ -442,7 +481,7 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
             while (mask) {
                 const int s = base + __builtin_ctzll(mask);
                 mask &= mask - 1;
-                test_sphere(S, s, r.start, d2, qa2, qa4, true, h);
+                test_sphere(S, s, r.start, d2, qa2, qa4, floor, true, h);
             }
         }
     } else if (!kPrimary && S.cull && S.nbvh > 0) {
@@ -456,7 +495,7 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
                 if (leaf) {
                     const int first = leaf & 0xFFFFFF, count = leaf >> 24;
                     for (int s = first; s < first + count; ++s)
-                        test_sphere(S, s, r.start, d2, qa2, qa4, false, h);
+                        test_sphere(S, s, r.start, d2, qa2, qa4, floor, false, h);
                     node = __float_as_int(lo.w);
                 } else {
                     node = node + 1;
@@ -466,7 +505,7 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
             }
         }
     } else {
-        for (int s = 0; s < S.ns; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, kPrimary, h);
+        for (int s = 0; s < S.ns; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, floor, kPrimary, h);
     }
     if (!valid) h.obj = -1;
     return h;
@@ -484,18 +523,14 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     const v3 d2 = muls(dir, 2.0f);
     const float qa = dot(dir, dir);
     const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
+    const float floor = root_floor(qa2);
     auto exact = [&](int s) {
         if (need && !hit) {
             const float4 c = S.sph[s];
             const v3 oc = sub(start, mk(c.x, c.y, c.z));
             const float qb = dot(d2, oc);
             const float qc = dot(oc, oc) - c.w;
-            const float qd = qb * qb - qa4 * qc;
-            if (qd >= 0.0f) {
-                bool inside;
-                const float t = sphere_t(qb, qc, qa2, qa4, inside);
-                hit = t > 0.0f && t < 1.0f;
-            }
+            hit = sphere_blocks(qb, qc, qa2, qa4, floor);
         }
     };
     if (!S.cull) {
