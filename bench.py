@@ -44,7 +44,6 @@ sys.path.insert(0, ROOT)
 WIDTH, HEIGHT, N_SPHERES, MAX_DEPTH = 1920, 1080, 16, 0
 BLOCK_ROWS = 8
 MC_SPP = 1024
-BYTES_PER_PIXEL = 16  # one float4 store per pixel (algorithmic HBM bytes)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "primary Mrays/s at 1920×1080; achieved HBM GB/s vs peak; 1/2/4/8-GPU scaling"
 
@@ -147,6 +146,8 @@ def main():
     sh = render_s.cuda_stream
     assert sh, "need a non-default HIP stream"
     mc = args.workload == "config5"
+    channels = 3 if (world > 1 and not mc) else 4
+    bytes_per_pixel = 4 * channels  # the render's store per pixel (algorithmic HBM bytes)
 
     if not mc:
         # N frames in flight, frame k = the orbit camera at t = k/60 s; every
@@ -154,13 +155,18 @@ def main():
         # launch (rt_render_batch); one all-to-all hands frame k's rows to
         # rank k (N gathers at once), which de-interleaves its frame. Double
         # buffered: the exchange of step i overlaps the render of step i+1.
+        # The shard buffers that travel are packed float3 (RT_OUTPUT_RGB32F:
+        # the alpha channel is the constant 0.0, raytrace_compute.glsl:404),
+        # 3/4 of the float4 bytes over xGMI; N=1 renders the float4 frame.
         n_frames = world
         views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
         rows_mine = HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
-        bufs = [torch.zeros(n_frames * rows_mine * WIDTH * 4, dtype=torch.float32, device="cuda")
+        if world > 1:
+            ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
+        bufs = [torch.zeros(n_frames * rows_mine * WIDTH * channels, dtype=torch.float32, device="cuda")
                 for _ in range(2 if world > 1 else 1)]
         if world > 1:
-            in_splits, out_splits = frame.exchange_splits(HEIGHT, WIDTH, BLOCK_ROWS, world, rank)
+            in_splits, out_splits = frame.exchange_splits(HEIGHT, WIDTH, BLOCK_ROWS, world, rank, channels=channels)
             recv = [torch.empty(sum(out_splits), dtype=torch.float32, device=coll_dev) for _ in bufs]
             perm = torch.as_tensor(frame.assembly_permutation(HEIGHT, BLOCK_ROWS, world), device=coll_dev)
             frames_out = [None, None]
@@ -220,7 +226,8 @@ def main():
         comm_s.wait_event(rendered[slot])
         src = bufs[slot] if coll_dev == "cuda" else bufs[slot].cpu()
         dist.all_to_all_single(recv[slot], src, out_splits, in_splits)  # frame k's rows -> rank k
-        frames_out[slot] = frame.assemble_frame(recv[slot], HEIGHT, WIDTH, BLOCK_ROWS, world, perm=perm)
+        frames_out[slot] = frame.assemble_frame(recv[slot], HEIGHT, WIDTH, BLOCK_ROWS, world, channels=channels,
+                                                perm=perm)
         e = torch.cuda.Event()
         e.record(comm_s)
         freed[slot] = e
@@ -251,7 +258,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = rays_per_step * args.steps / elapsed / 1e6
     avg_kernel_ms = float(np.mean(kernel_ms))
-    achieved = px_per_launch * BYTES_PER_PIXEL / (avg_kernel_ms * 1e-3) / 1e9
+    achieved = px_per_launch * bytes_per_pixel / (avg_kernel_ms * 1e-3) / 1e9
     pmc = pmc_latest(args.workload) if world == 1 else {}
     traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
@@ -263,6 +270,7 @@ def main():
                                     "(primary + shadow rays)",
                         "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES, "max_depth": MAX_DEPTH,
                         "frames_per_step": n_frames, "row_block": BLOCK_ROWS,
+                        "output": "float4 frame" if world == 1 else "float3 shards (alpha 0 dropped) exchanged",
                         "parallelism": ("row-tiles x%d + RCCL all-to-all frame exchange (frame k gathered to "
                                         "rank k), overlapped with the next render" % world)
                                        if world > 1 else "single GPU"}
@@ -289,7 +297,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_ms, 5),
-                         "bytes_per_launch": px_per_launch * BYTES_PER_PIXEL,
+                         "bytes_per_launch": px_per_launch * bytes_per_pixel,
                          "valu": valu_bound(pmc, avg_kernel_ms)},
             "cpu_baseline": cpu,
         }

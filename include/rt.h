@@ -240,10 +240,14 @@ int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *
  * kernel packs each pixel in its epilogue — clamp to [0, 1], unorm rounding,
  * exactly rt_pack_rgba8 of the float frame — and stores 4 bytes per pixel, so
  * every `out` buffer then holds width*rows*4 bytes (uint8 r, g, b, a).
- * rt_render_accumulate keeps float sums and refuses RGBA8. */
+ * RT_OUTPUT_RGB32F drops the alpha channel, which is always 0.0 (:404): 3
+ * floats per pixel (width*rows*12 bytes), the compact transport form of a
+ * float frame (the multi-GPU frame exchange ships 3/4 of the bytes).
+ * rt_render_accumulate keeps float4 sums and refuses the other formats. */
 #define RT_OPT_OUTPUT 3
 #define RT_OUTPUT_RGBA32F 0
 #define RT_OUTPUT_RGBA8 1
+#define RT_OUTPUT_RGB32F 2
 int rt_context_set(rt_context *ctx, int option, int value);
 
 /* Kernel-only timing of the last render call (ms, from HIP events around the

@@ -212,8 +212,9 @@ class Context:
         _check(lib().rt_context_set(self._h, abi.RT_OPT_TIMING, 1 if on else 0))
 
     def set_output(self, fmt):
-        """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel) or
-        abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)."""
+        """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel),
+        abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)
+        or abi.RT_OUTPUT_RGB32F (packed float3, the constant alpha dropped)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_OUTPUT, fmt))
         self.output = fmt
 

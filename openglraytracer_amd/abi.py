@@ -23,6 +23,7 @@ RT_OPT_TIMING = 2
 RT_OPT_OUTPUT = 3
 RT_OUTPUT_RGBA32F = 0
 RT_OUTPUT_RGBA8 = 1
+RT_OUTPUT_RGB32F = 2
 RT_MAX_BATCH = 8
 
 # material indices of the reference table (raytrace_compute.glsl:74-157)

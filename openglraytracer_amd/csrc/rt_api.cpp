@@ -87,7 +87,7 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.off_lightmat = d.off_lightmat;
     p.off_bvh = d.off_bvh;
     p.off_cone = d.off_cone;
-    p.out_rgba8 = ctx->output == RT_OUTPUT_RGBA8 ? 1 : 0;
+    p.out_format = ctx->output;
     p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
     host_frame_setup(p, scene->host.empty() ? nullptr : scene->host.data());
@@ -274,7 +274,7 @@ int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, 
     p.n_rows = row_end - row_begin;
     const size_t n_px = static_cast<size_t>(p.n_rows) * width;
     hipStream_t stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->stream;
-    const size_t px_bytes = p.out_rgba8 ? 4 : sizeof(float4);
+    const size_t px_bytes = p.out_format == RT_OUTPUT_RGBA8 ? 4 : (p.out_format == RT_OUTPUT_RGB32F ? 12 : sizeof(float4));
     if (out_is_device) {
         p.out = reinterpret_cast<float4 *>(out);
     } else {
@@ -282,7 +282,7 @@ int rt_render_view(rt_context *ctx, const rt_scene *scene, const rt_view *view, 
             if (ctx->staging) (void)hipFree(ctx->staging);
             ctx->staging = nullptr;
             ctx->staging_px = 0;
-            e = hipMalloc(&ctx->staging, n_px * sizeof(float4));  // sized for float: serves both formats
+            e = hipMalloc(&ctx->staging, n_px * sizeof(float4));  // sized for float4: serves every format
             if (e != hipSuccess) return hip_fail("hipMalloc(staging)", e);
             ctx->staging_px = n_px;
         }
@@ -473,7 +473,7 @@ int rt_context_set(rt_context *ctx, int option, int value) {
         case RT_OPT_CULLING: ctx->culling = value ? 1 : 0; return RT_OK;
         case RT_OPT_TIMING: ctx->timing = value ? 1 : 0; return RT_OK;
         case RT_OPT_OUTPUT:
-            if (value != RT_OUTPUT_RGBA32F && value != RT_OUTPUT_RGBA8) {
+            if (value != RT_OUTPUT_RGBA32F && value != RT_OUTPUT_RGBA8 && value != RT_OUTPUT_RGB32F) {
                 set_error("rt_context_set: unknown output format " + std::to_string(value));
                 return RT_ERR_INVALID;
             }

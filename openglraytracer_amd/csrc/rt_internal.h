@@ -132,7 +132,7 @@ struct LaunchParams {
     // per tile.
     int32_t *sched;
     int32_t n_cu;
-    int32_t out_rgba8;  // 1: store GL_RGBA8 unorm bytes (uchar4 per pixel) instead of float4
+    int32_t out_format;  // RT_OUTPUT_*: float4, GL_RGBA8 unorm bytes (uchar4) or packed float3 per pixel
     // The view's per-frame constants ([sphere camera terms][sphere pixel
     // footprints][box camera terms], the LDS image the kernel's frame_setup
     // derives), computed on the host when a one-view launch's fit here

@@ -696,7 +696,15 @@ __device__ unsigned long long rt_phase_buf[kPhaseWaves * 16];
         const unsigned wg_ = (blockIdx.y * gridDim.x + blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6); \
         if ((threadIdx.x & 63) == 0 && wg_ < kPhaseWaves) rt_phase_buf[wg_ * 16 + (k)] = now_;              \
     } while (0)
+// the clock read after `v` is available (a branch on it orders the read)
+#define RT_PHASE_AFTER(k, v)                     \
+    do {                                         \
+        if ((v) != -123456789) RT_PHASE(k);      \
+    } while (0)
 #else
+#define RT_PHASE_AFTER(k, v) \
+    do {                     \
+    } while (0)
 #define RT_PHASE(k) \
     do {            \
     } while (0)
@@ -897,9 +905,14 @@ __device__ __forceinline__ uint32_t unorm8(float v) {
 // One pixel's colour into the launch's surface (float4 or GL_RGBA8 bytes).
 __device__ __forceinline__ void store_pixel(const LaunchParams &p, int z, size_t idx, v3 col) {
     const size_t at = static_cast<size_t>(z) * p.n_rows * p.width + idx;
-    if (p.out_rgba8)  // GL_RGBA8 unorm store of vec4(rgb, 0.0) (main.cpp:223, :404): rt_pack_rgba8
+    if (p.out_format == RT_OUTPUT_RGBA8) {  // GL_RGBA8 unorm store of vec4(rgb, 0.0) (main.cpp:223, :404): rt_pack_rgba8
         reinterpret_cast<uint32_t *>(p.out)[at] = unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16);
-    else
+    } else if (p.out_format == RT_OUTPUT_RGB32F) {  // packed float3, the constant alpha dropped
+        float *o = reinterpret_cast<float *>(p.out) + 3 * at;
+        o[0] = col.x;
+        o[1] = col.y;
+        o[2] = col.z;
+    } else
         p.out[at] = make_float4(col.x, col.y, col.z, 0.0f);
 }
 
@@ -1157,8 +1170,10 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     const int own_wx = static_cast<int>(blockIdx.x) * kWavesX + wave % kWavesX;
     const int own_wy = static_cast<int>(blockIdx.y) * kWavesY + wave / kWavesX;
     const Pixel own = wave_pixel(p, own_wx, own_wy);
+    RT_PHASE_AFTER(14, own.y);
     Ray own_ray;
     if (!queued && !kAccum) own_ray = camera_ray(p, V, own.x, own.y, 0.0f, 0.0f);
+    RT_PHASE_AFTER(15, own_ray.dir.x + own_ray.dir.y + own_ray.dir.z);
     RT_PHASE(10);
     if (tid < p.blob_units) lds[tid] = first;
     RT_PHASE(11);

@@ -68,14 +68,15 @@ def exchange_worker(rank, world, port, result_path):
     objs = scenes.bench_objects(16)
     times = [k / 60.0 for k in range(world)]  # one frame per rank in flight
     ids = frame.shard_row_ids(H, BLOCK, world, rank)
-    # the batch buffer rt_render_batch writes: (frames, this shard's rows, W, 4)
+    # the batch buffer rt_render_batch writes in bench.py's exchange format
+    # (RT_OUTPUT_RGB32F): (frames, this shard's rows, W, 3)
     data = np.stack([np.concatenate([oracle_port.render(objs, W, H, DEPTH, t, rows=(int(r), int(r) + 1))
-                                     for r in ids]) for t in times])
+                                     for r in ids]) for t in times])[..., :3]
     send = torch.from_numpy(np.ascontiguousarray(data).reshape(-1))
-    in_splits, out_splits = frame.exchange_splits(H, W, BLOCK, world, rank)
+    in_splits, out_splits = frame.exchange_splits(H, W, BLOCK, world, rank, channels=3)
     recv = torch.empty(sum(out_splits), dtype=torch.float32)
     dist.all_to_all_single(recv, send, out_splits, in_splits)  # frame k's rows -> rank k
-    np.save(result_path + ".%d.npy" % rank, frame.assemble_frame(recv, H, W, BLOCK, world).numpy())
+    np.save(result_path + ".%d.npy" % rank, frame.assemble_frame(recv, H, W, BLOCK, world, channels=3).numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -84,13 +85,15 @@ def exchange_worker(rank, world, port, result_path):
 def test_exchange_assembles_one_frame_per_rank(tmp_path, world):
     """bench.py's N-GPU frame exchange: N frames in flight, every rank renders
     its row blocks of all of them, one all-to-all delivers frame k's rows to
-    rank k, which de-interleaves it — bit-identical to the whole frame."""
+    rank k, which de-interleaves it — bit-identical to the whole frame's rgb
+    (the shards travel as packed float3; alpha is the constant 0)."""
     from oracle import port as oracle_port, scenes
     out = str(tmp_path / "frame")
     mp.start_processes(exchange_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
     for k in range(world):
         full = oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, k / 60.0)
-        assert np.array_equal(np.load(out + ".%d.npy" % k), full), k
+        assert (full[..., 3] == 0).all()
+        assert np.array_equal(np.load(out + ".%d.npy" % k), full[..., :3]), k
 
 
 def mc_worker(rank, world, port, result_path):

@@ -435,6 +435,44 @@ def test_rgba8_surface_equals_packed_float_frame(gpu_ctx, cfg, w, h):
         sc.close()
 
 
+@pytest.mark.parametrize("n_shards", [1, 2, 8])
+def test_rgb32f_exchange_format_equals_float_frames(gpu_ctx, n_shards):
+    """RT_OUTPUT_RGB32F (the multi-GPU exchange's transport form): packed
+    float3 per pixel == the rgb of the float4 frame, bit for bit, for whole
+    frames and for every shard's rows of a batch launch (bench.py's path);
+    the exchange + assembly on 3 channels rebuilds each frame."""
+    objs = scenes.bench_objects(16)
+    w, h, block = 320, 180, 8
+    views = [rt.make_view(None, k / 60.0) for k in range(n_shards)]
+    sc = rt.Scene(gpu_ctx, objs)
+    singles = [rt.render(gpu_ctx, sc, w, h, 0, view=v) for v in views]
+    gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
+    try:
+        one = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+        rt.render_device(gpu_ctx, sc, one.data_ptr(), w, h, 0, view=views[0])
+        torch.cuda.synchronize()
+        assert np.array_equal(one.cpu().numpy(), singles[0][..., :3])
+        bufs = []
+        for shard in range(n_shards):
+            rows = frame.shard_row_ids(h, block, n_shards, shard)
+            out = torch.zeros((n_shards, len(rows), w, 3), dtype=torch.float32, device="cuda")
+            rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, 0, views, block, n_shards, shard)
+            got = out.cpu().numpy()
+            for k in range(n_shards):
+                assert np.array_equal(got[k], singles[k][rows][..., :3]), (shard, k)
+            bufs.append(out.reshape(-1))
+        # the all-to-all by hand: rank k receives frame k's rows of every shard
+        for k in range(n_shards):
+            ins = [frame.exchange_splits(h, w, block, n_shards, s, channels=3)[0] for s in range(n_shards)]
+            recv = torch.cat([bufs[s][k * ins[s][k]:(k + 1) * ins[s][k]] for s in range(n_shards)])
+            assert recv.numel() == sum(frame.exchange_splits(h, w, block, n_shards, k, channels=3)[1])
+            fr = frame.assemble_frame(recv, h, w, block, n_shards, channels=3).cpu().numpy()
+            assert np.array_equal(fr, singles[k][..., :3])
+    finally:
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA32F)
+        sc.close()
+
+
 def test_cli_renders_a_scene_description(gpu_ctx, tmp_path):
     """rt_cli (the headless main()/draw() driver) on scenes/config1.json: its
     PPM is the RGBA8 surface of the same frame rendered through the C-ABI."""

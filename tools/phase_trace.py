@@ -109,6 +109,9 @@ print("waves started in the first 5 us per CU: min %d max %d mean %.2f" % (cnt.m
 P = (R[:, 10:14] - t0) * us
 print("prologue split (us): entry->raygen %.2f, raygen->blob in LDS %.2f, ->frame_setup done %.2f, barrier wait %.2f"
       % tuple(np.diff(np.concatenate([T[:, :1], P], axis=1), axis=1).mean(axis=0)))
+Q = (R[:, 14:16] - t0) * us
+print("entry split (us): entry->own pixel (kernargs) %.2f, ->camera ray done %.2f, ->phase 10 %.2f"
+      % ((Q[:, 0] - T[:, 0]).mean(), (Q[:, 1] - Q[:, 0]).mean(), (P[:, 0] - Q[:, 1]).mean()))
 w = np.arange(waves) % 4
 for k in range(4):
     m = w == k
