@@ -248,6 +248,12 @@ int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *
 #define RT_OUTPUT_RGBA32F 0
 #define RT_OUTPUT_RGBA8 1
 #define RT_OUTPUT_RGB32F 2
+/* RT_OPT_FRAME_CONSTS (default 1): a launch's per-frame constants (every
+ * sphere's and box's camera-origin terms and every sphere's pixel footprint,
+ * per view) are computed on the host and carried in the kernel arguments when
+ * all views' records fit (144 records: e.g. 4 views of 16 spheres + 1 box);
+ * 0: every work-group derives them on the device. Output is identical. */
+#define RT_OPT_FRAME_CONSTS 4
 int rt_context_set(rt_context *ctx, int option, int value);
 
 /* Kernel-only timing of the last render call (ms, from HIP events around the

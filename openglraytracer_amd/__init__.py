@@ -211,6 +211,11 @@ class Context:
         """RT_OPT_TIMING: HIP events around every launch (for last_kernel_ms)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_TIMING, 1 if on else 0))
 
+    def set_host_frame_consts(self, on):
+        """RT_OPT_FRAME_CONSTS: per-frame constants from the host when they fit
+        (default), else derived by every work-group (output identical)."""
+        _check(lib().rt_context_set(self._h, abi.RT_OPT_FRAME_CONSTS, 1 if on else 0))
+
     def set_output(self, fmt):
         """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel),
         abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)

@@ -90,7 +90,11 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.out_format = ctx->output;
     p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
-    host_frame_setup(p, scene->host.empty() ? nullptr : scene->host.data());
+    if (ctx->host_consts) {
+        const float4 *blobs[kMaxViews];
+        for (int k = 0; k < n_views; ++k) blobs[k] = scene->host.empty() ? nullptr : scene->host.data();
+        host_frame_setup(p, blobs);
+    }
     return p;
 }
 
@@ -391,6 +395,11 @@ int render_batch_impl(rt_context *ctx, const rt_scene *const *scenes, const rt_v
         }
         p.view[k].blob = scenes[k]->dev.blob;
     }
+    if (ctx->host_consts) {  // each view's constants from its own scene
+        const float4 *blobs[kMaxViews];
+        for (int k = 0; k < n_views; ++k) blobs[k] = scenes[k]->host.empty() ? nullptr : scenes[k]->host.data();
+        host_frame_setup(p, blobs);
+    }
     p.row_begin = 0;
     p.n_rows = rows;
     if (sharded) {
@@ -472,6 +481,7 @@ int rt_context_set(rt_context *ctx, int option, int value) {
     switch (option) {
         case RT_OPT_CULLING: ctx->culling = value ? 1 : 0; return RT_OK;
         case RT_OPT_TIMING: ctx->timing = value ? 1 : 0; return RT_OK;
+        case RT_OPT_FRAME_CONSTS: ctx->host_consts = value ? 1 : 0; return RT_OK;
         case RT_OPT_OUTPUT:
             if (value != RT_OUTPUT_RGBA32F && value != RT_OUTPUT_RGBA8 && value != RT_OUTPUT_RGB32F) {
                 set_error("rt_context_set: unknown output format " + std::to_string(value));

@@ -133,10 +133,11 @@ struct LaunchParams {
     int32_t *sched;
     int32_t n_cu;
     int32_t out_format;  // RT_OUTPUT_*: float4, GL_RGBA8 unorm bytes (uchar4) or packed float3 per pixel
-    // The view's per-frame constants ([sphere camera terms][sphere pixel
+    // Each view's per-frame constants ([sphere camera terms][sphere pixel
     // footprints][box camera terms], the LDS image the kernel's frame_setup
-    // derives), computed on the host when a one-view launch's fit here
-    // (host_frame_setup); 0: every work-group derives them.
+    // derives), computed on the host when all views' fit here
+    // (host_frame_setup): n_frame_consts records per view, view k's at
+    // k * n_frame_consts; 0: every work-group derives them.
     int32_t n_frame_consts;
     float4 frame_consts[kMaxFrameConsts];
 };
@@ -154,12 +155,13 @@ struct DeviceScene {
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
 
-// rt_scene.cpp: the view's per-frame constants on the host, bit-identical to
-// the kernel's frame_setup for the camera terms (float32, same operation
-// order) and conservative pixel footprints; writes 2 * n_spheres + n_boxes
-// records into p.frame_consts and sets p.n_frame_consts, or leaves 0 when
-// they do not fit.
-void host_frame_setup(LaunchParams &p, const float4 *blob);
+// rt_scene.cpp: every view's per-frame constants on the host, bit-identical
+// to the kernel's frame_setup for the camera terms (float32, same operation
+// order) and conservative pixel footprints; view k's 2 * n_spheres + n_boxes
+// records (from its scene's host blob, blobs[k]) go to p.frame_consts at
+// k * p.n_frame_consts, p.n_frame_consts = records per view, or 0 when they
+// do not all fit.
+void host_frame_setup(LaunchParams &p, const float4 *const *blobs);
 
 // rt_kernel.hip
 hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t stream);
@@ -180,6 +182,7 @@ struct rt_context {
     int culling = 1;  // RT_OPT_CULLING
     int timing = 1;   // RT_OPT_TIMING
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
+    int host_consts = 1;  // RT_OPT_FRAME_CONSTS
     int n_cu = 0;               // compute units of the device
     int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
     unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots

@@ -1160,10 +1160,11 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     const int tid = threadIdx.x;
     float4 first = make_float4(0.0f, 0.0f, 0.0f, 0.0f), fc = first;
     if (tid < p.blob_units) first = blob[tid];
-    // per-frame constants computed on the host (one-view launches, small
-    // scenes: host_frame_setup) — else derived below by every work-group
+    // this view's per-frame constants computed on the host (when every
+    // view's fit in the kernel arguments: host_frame_setup) — else derived
+    // below by every work-group
     static_assert(kMaxFrameConsts <= kThreads, "one record per thread");
-    if (tid < p.n_frame_consts) fc = p.frame_consts[tid];
+    if (tid < p.n_frame_consts) fc = p.frame_consts[z * p.n_frame_consts + tid];
     float4 *sph_cam = lds + p.blob_units;
     int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
     float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);

@@ -425,11 +425,21 @@ bool view_projection(const rt_view &v, float proj[16]) {
 // LDS image is bit-identical; footprints in float64 with the same inflation
 // and 2-pixel margin — closer to the exact projection than the kernel's
 // approximate-reciprocal version, and as conservative.
-void host_frame_setup(LaunchParams &p, const float4 *blob) {
+static void view_frame_setup(const LaunchParams &p, const FrameView &V, const float4 *blob, float4 *out);
+
+void host_frame_setup(LaunchParams &p, const float4 *const *blobs) {
     p.n_frame_consts = 0;
+    const int ns = p.n_spheres, nb = p.n_boxes, per = 2 * ns + nb;
+    if (per == 0 || p.n_views < 1 || p.n_views * per > kMaxFrameConsts) return;
+    for (int k = 0; k < p.n_views; ++k)
+        if (!blobs[k]) return;
+    for (int k = 0; k < p.n_views; ++k) view_frame_setup(p, p.view[k], blobs[k], p.frame_consts + k * per);
+    p.n_frame_consts = per;
+}
+
+// One view's records (host_frame_setup).
+static void view_frame_setup(const LaunchParams &p, const FrameView &V, const float4 *blob, float4 *out) {
     const int ns = p.n_spheres, nb = p.n_boxes;
-    if (p.n_views != 1 || !blob || 2 * ns + nb > kMaxFrameConsts || 2 * ns + nb == 0) return;
-    const FrameView &V = p.view[0];
     const float ox = V.origin[0], oy = V.origin[1], oz = V.origin[2];
     const int hw = p.width / 2, hh = p.height / 2;
     const bool cull = V.cull && hw > 0 && hh > 0;
@@ -437,7 +447,7 @@ void host_frame_setup(LaunchParams &p, const float4 *blob) {
     const auto *sph = reinterpret_cast<const SphereRec *>(blob + p.off_spheres);
     const auto *meta = reinterpret_cast<const SphereMeta *>(blob + p.off_smeta);
     const auto *box = reinterpret_cast<const BoxRec *>(blob + p.off_boxes);
-    float4 *cam = p.frame_consts, *px = p.frame_consts + ns, *bcam = p.frame_consts + 2 * ns;
+    float4 *cam = out, *px = out + ns, *bcam = out + 2 * ns;
     for (int s = 0; s < ns; ++s) {
         const SphereRec c = sph[s];
         const float ocx = ox - c.cx, ocy = oy - c.cy, ocz = oz - c.cz;
@@ -480,7 +490,6 @@ void host_frame_setup(LaunchParams &p, const float4 *blob) {
                             rz < B.maxs[2];
         bcam[b] = make_float4(rx, ry, rz, inside ? 1.0f : 0.0f);
     }
-    p.n_frame_consts = 2 * ns + nb;
 }
 
 // Build the device blob: [spheres][sphere meta][boxes][materials][lights]

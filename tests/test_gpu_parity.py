@@ -156,10 +156,10 @@ def _inside_sphere_camera():
 
 @pytest.mark.parametrize("case", ["bench16", "bench64", "shipped", "inside_sphere", "no_culling"])
 def test_host_frame_constants_equal_device_ones(gpu_ctx, case):
-    """A one-view launch takes its per-frame constants from the host
-    (host_frame_setup, carried in the kernel arguments); a batch launch
-    derives them in every work-group (frame_setup). Both must give the same
-    frame, bit for bit — camera terms identical, footprints conservative."""
+    """Per-frame constants from the host (host_frame_setup, carried in the
+    kernel arguments, per view of a batch when they all fit) or derived in
+    every work-group (frame_setup, RT_OPT_FRAME_CONSTS = 0): the same frames,
+    bit for bit — camera terms identical, footprints conservative."""
     w, h, depth, cam = 256, 144, 1, None
     if case in ("bench16", "no_culling"):
         objs, view_t = scenes.bench_objects(16), 0.4
@@ -175,13 +175,23 @@ def test_host_frame_constants_equal_device_ones(gpu_ctx, case):
     try:
         sc = rt.Scene(gpu_ctx, objs)
         single = rt.render(gpu_ctx, sc, w, h, depth, view=view)
-        out = torch.zeros((2, h, w, 4), dtype=torch.float32, device="cuda")
-        rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, [view, view])
-        got = out.cpu().numpy()
+        other = rt.make_view(cam, view_t + 0.7) if cam is None else view
+        other_single = rt.render(gpu_ctx, sc, w, h, depth, view=other)
+        got = {}
+        for host in (True, False):
+            gpu_ctx.set_host_frame_consts(host)
+            out = torch.zeros((2, h, w, 4), dtype=torch.float32, device="cuda")
+            rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, [view, other])
+            got[host] = out.cpu().numpy()
+            if not host:
+                dev_single = rt.render(gpu_ctx, sc, w, h, depth, view=view)
         sc.close()
     finally:
         gpu_ctx.set_culling(True)
-    assert np.array_equal(got[0], single) and np.array_equal(got[1], single)
+        gpu_ctx.set_host_frame_consts(True)
+    assert np.array_equal(dev_single, single)
+    for host in (True, False):
+        assert np.array_equal(got[host][0], single) and np.array_equal(got[host][1], other_single), host
     if case in ("bench16", "shipped"):
         o = oracle_render(objs, w, h, depth, view_t)
         assert np.array_equal(single, o), parity_stats(single, o)
