@@ -251,7 +251,8 @@ int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *
 /* RT_OPT_FRAME_CONSTS (default 1): a launch's per-frame constants (every
  * sphere's and box's camera-origin terms and every sphere's pixel footprint,
  * per view) are computed on the host and carried in the kernel arguments when
- * all views' records fit (144 records: e.g. 4 views of 16 spheres + 1 box);
+ * all views' records fit (272 records, at most 256 per view: e.g. 8 views of
+ * 16 spheres + 1 box);
  * 0: every work-group derives them on the device. Output is identical. */
 #define RT_OPT_FRAME_CONSTS 4
 int rt_context_set(rt_context *ctx, int option, int value);

@@ -1163,7 +1163,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // this view's per-frame constants computed on the host (when every
     // view's fit in the kernel arguments: host_frame_setup) — else derived
     // below by every work-group
-    static_assert(kMaxFrameConsts <= kThreads, "one record per thread");
+    static_assert(kMaxViewConsts <= kThreads, "one record per thread");
     if (tid < p.n_frame_consts) fc = p.frame_consts[z * p.n_frame_consts + tid];
     float4 *sph_cam = lds + p.blob_units;
     int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);

@@ -430,7 +430,7 @@ static void view_frame_setup(const LaunchParams &p, const FrameView &V, const fl
 void host_frame_setup(LaunchParams &p, const float4 *const *blobs) {
     p.n_frame_consts = 0;
     const int ns = p.n_spheres, nb = p.n_boxes, per = 2 * ns + nb;
-    if (per == 0 || p.n_views < 1 || p.n_views * per > kMaxFrameConsts) return;
+    if (per == 0 || per > kMaxViewConsts || p.n_views < 1 || p.n_views * per > kMaxFrameConsts) return;
     for (int k = 0; k < p.n_views; ++k)
         if (!blobs[k]) return;
     for (int k = 0; k < p.n_views; ++k) view_frame_setup(p, p.view[k], blobs[k], p.frame_consts + k * per);
