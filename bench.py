@@ -4,15 +4,20 @@ Default workload (BASELINE.json configs[1]):
 1920x1080, room box + 16 seeded spheres, the reference's 3 lights and 7
 materials, max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
 
-A step renders N frames of 1920x1080 (N = number of GPUs; frame k is the
-reference orbit camera at time k/60 s). Every frame is row-tiled across the N
-ranks in interleaved 8-row blocks; each rank renders its blocks of all N
-frames in one launch (rt_render_batch), and one RCCL all-to-all over xGMI
-gathers frame k to rank k (N gathers at once, every link carrying 1/N of the
-frame traffic), which de-interleaves its rows into the assembled frame. The
-exchange of step i runs on its own stream beside the render of step i+1
-(double-buffered). Per-GPU work is one frame per step at every N: weak
-scaling. At N=1 a step is one full frame rendered in place (no collective).
+A step is the animated frame loop (main.cpp:81-86): F frames of 1920x1080
+per GPU (--frames-per-gpu, default 8; frame k is the reference orbit camera at
+time k/60 s), rendered up to 8 frames per launch (rt_render_batch; SURVEY.md
+§8(f) row 3 — several frames per launch amortise the launch ramp-up and
+tail). On N GPUs a step holds N*F frames: every frame is row-tiled across the
+N ranks in interleaved 8-row blocks, each rank renders its blocks of all N*F
+frames, and one RCCL all-to-all over xGMI hands frames [kF, (k+1)F) to rank k
+(N gathers at once, every link carrying 1/N of the frame traffic), which
+de-interleaves its rows into the assembled frames. The shards travel as
+packed float3 (the alpha channel is the constant 0). The exchange of step i
+runs on its own stream beside the render of step i+1 (double-buffered).
+Per-GPU work is F frames per step at every N: weak scaling. At N=1 the frames
+are rendered in place (float4, no collective). --frames-per-gpu 1 gives the
+single-frame launch.
 
 --workload config5 (a Monte-Carlo extension the
 reference does not have): one step = the 1920x1080 frame at 1024 jittered
@@ -54,6 +59,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["config2", "config5"], default="config2")
+    ap.add_argument("--frames-per-gpu", type=int, default=8,
+                    help="config2: animated frames each GPU renders per step, up to 8 per launch "
+                         "(rt_render_batch; SURVEY.md §8(f) row 3)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -81,14 +89,16 @@ def cpu_baseline(budget_s):
     return None
 
 
-def pmc_latest(workload):
+def pmc_latest(workload, frames_per_launch):
     """The committed PMC summary of the render kernel (profiles/pmc_latest.json,
-    written by tools/pmc_summary.py) for this workload at N=1, or {}."""
+    written by tools/pmc_summary.py) for this workload and launch shape at
+    N=1, or {}."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == workload and d.get("n_gpus", 1) == 1:
+        if (d.get("workload") == workload and d.get("n_gpus", 1) == 1
+                and d.get("frames_per_launch", 1) == frames_per_launch):
             return d
     except (OSError, ValueError):
         pass
@@ -157,21 +167,34 @@ def main():
         # buffered: the exchange of step i overlaps the render of step i+1.
         # The shard buffers that travel are packed float3 (RT_OUTPUT_RGB32F:
         # the alpha channel is the constant 0.0, raytrace_compute.glsl:404),
-        # 3/4 of the float4 bytes over xGMI; N=1 renders the float4 frame.
-        n_frames = world
+        # 3/4 of the float4 bytes over xGMI; N=1 renders float4 frames.
+        # A step is the animated frame loop (main.cpp:81-86) F frames per
+        # GPU: N*F frames at t = k/60 s, rank k's frames [kF, (k+1)F).
+        fpg = args.frames_per_gpu
+        n_frames = world * fpg
         views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
         rows_mine = HEIGHT if world == 1 else rt.shard_rows(HEIGHT, BLOCK_ROWS, world, rank)
         if world > 1:
             ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
         bufs = [torch.zeros(n_frames * rows_mine * WIDTH * channels, dtype=torch.float32, device="cuda")
                 for _ in range(2 if world > 1 else 1)]
+        # launches of up to RT_MAX_BATCH views: (first frame, views) each
+        chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, n_frames, rt.abi.RT_MAX_BATCH)]
+        frame_elems = rows_mine * WIDTH * channels
         if world > 1:
-            in_splits, out_splits = frame.exchange_splits(HEIGHT, WIDTH, BLOCK_ROWS, world, rank, channels=channels)
+            in_splits, out_splits = frame.exchange_splits(HEIGHT, WIDTH, BLOCK_ROWS, world, rank, channels=channels,
+                                                          frames_per_rank=fpg)
             recv = [torch.empty(sum(out_splits), dtype=torch.float32, device=coll_dev) for _ in bufs]
-            perm = torch.as_tensor(frame.assembly_permutation(HEIGHT, BLOCK_ROWS, world), device=coll_dev)
+            idx = torch.as_tensor(frame.assembly_rows(HEIGHT, BLOCK_ROWS, world, fpg), device=coll_dev)
             frames_out = [None, None]
-        px_per_launch = WIDTH * rows_mine * n_frames
+        launches_per_step = len(chunks)
+        px_per_launch = WIDTH * rows_mine * n_frames // launches_per_step
         rays_per_step = n_frames * WIDTH * HEIGHT
+
+        def render_frames(buf):
+            for j, vs in chunks:
+                rt.render_batch(ctx, scene, buf.data_ptr() + 4 * j * frame_elems, WIDTH, HEIGHT, MAX_DEPTH, vs,
+                                BLOCK_ROWS, world, rank, stream=sh)
     else:
         view = rt.make_view(None, 0.0)
         spp_mine = MC_SPP // world + (1 if rank < MC_SPP % world else 0)
@@ -179,11 +202,12 @@ def main():
         accum = torch.zeros((HEIGHT, WIDTH, 4), dtype=torch.float32, device="cuda")
         px_per_launch = WIDTH * HEIGHT
         rays_per_step = MC_SPP * WIDTH * HEIGHT
+        launches_per_step = 1
 
     # Kernel time from HIP events on the render stream. At N=1 (config 2) a
-    # step is exactly one render launch: one event pair brackets the K
-    # back-to-back launches of the timed region (no markers between frames);
-    # otherwise a pair brackets every render launch.
+    # step is its render launches alone: one event pair brackets the
+    # back-to-back launches of the whole timed region (no markers between
+    # frames); otherwise a pair brackets every step's render launches.
     per_launch = world > 1 or mc
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps if per_launch else 1)]
@@ -209,25 +233,23 @@ def main():
             if rank == 0:
                 total.mul_(1.0 / MC_SPP)  # the estimate: mean over all samples
             return
-        if world == 1:  # one frame rendered in place, launches back to back
-            rt.render_batch(ctx, scene, bufs[0].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS, 1, 0,
-                            stream=sh)
+        if world == 1:  # the frames rendered in place, launches back to back
+            render_frames(bufs[0])
             return
         slot = it % 2
         if freed[slot] is not None:
             render_s.wait_event(freed[slot])  # the exchange of step it-2 has read bufs[slot]
         if timed:
             ev[it][0].record(render_s)
-        rt.render_batch(ctx, scene, bufs[slot].data_ptr(), WIDTH, HEIGHT, MAX_DEPTH, views, BLOCK_ROWS, world,
-                        rank, stream=sh)
+        render_frames(bufs[slot])
         if timed:
             ev[it][1].record(render_s)
         rendered[slot].record(render_s)
         comm_s.wait_event(rendered[slot])
         src = bufs[slot] if coll_dev == "cuda" else bufs[slot].cpu()
-        dist.all_to_all_single(recv[slot], src, out_splits, in_splits)  # frame k's rows -> rank k
-        frames_out[slot] = frame.assemble_frame(recv[slot], HEIGHT, WIDTH, BLOCK_ROWS, world, channels=channels,
-                                                perm=perm)
+        dist.all_to_all_single(recv[slot], src, out_splits, in_splits)  # frames [kF, (k+1)F) -> rank k
+        frames_out[slot] = frame.assemble_frames(recv[slot], fpg, HEIGHT, WIDTH, BLOCK_ROWS, world,
+                                                 channels=channels, idx=idx)
         e = torch.cuda.Event()
         e.record(comm_s)
         freed[slot] = e
@@ -250,7 +272,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kernel_ms = [a.elapsed_time(b) for a, b in ev] if per_launch else [ev[0][0].elapsed_time(ev[0][1]) / args.steps]
+    kernel_ms = ([a.elapsed_time(b) / launches_per_step for a, b in ev] if per_launch else
+                 [ev[0][0].elapsed_time(ev[0][1]) / (args.steps * launches_per_step)])
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -259,7 +282,7 @@ def main():
     value = rays_per_step * args.steps / elapsed / 1e6
     avg_kernel_ms = float(np.mean(kernel_ms))
     achieved = px_per_launch * bytes_per_pixel / (avg_kernel_ms * 1e-3) / 1e9
-    pmc = pmc_latest(args.workload) if world == 1 else {}
+    pmc = pmc_latest(args.workload, 1 if mc else n_frames // launches_per_step) if world == 1 else {}
     traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
         cpu = None
@@ -269,7 +292,8 @@ def main():
             workload = {"workload": "config2: 1920x1080, room box + 16 spheres, max_depth 0 "
                                     "(primary + shadow rays)",
                         "width": WIDTH, "height": HEIGHT, "spheres": N_SPHERES, "max_depth": MAX_DEPTH,
-                        "frames_per_step": n_frames, "row_block": BLOCK_ROWS,
+                        "frames_per_step": n_frames, "frames_per_gpu": fpg,
+                        "frames_per_launch": n_frames // launches_per_step, "row_block": BLOCK_ROWS,
                         "output": "float4 frame" if world == 1 else "float3 shards (alpha 0 dropped) exchanged",
                         "parallelism": ("row-tiles x%d + RCCL all-to-all frame exchange (frame k gathered to "
                                         "rank k), overlapped with the next render" % world)

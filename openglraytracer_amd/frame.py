@@ -64,13 +64,51 @@ def assemble(flat, n_frames, height, width, block_rows, channels=4, perm=None):
     return np.concatenate(parts, axis=1)[:, perm]
 
 
-def exchange_splits(height, width, block_rows, n_shards, rank, channels=4):
+def exchange_splits(height, width, block_rows, n_shards, rank, channels=4, frames_per_rank=1):
     """All-to-all split sizes (elements) for the frame exchange: this rank's
-    batch buffer is (n_shards frames, rows_rank, width, channels), frame k's
-    rows going to rank k; it receives its own frame's rows from every shard,
-    concatenated in shard order. Returns (input_splits, output_splits)."""
+    batch buffer is (n_shards * F frames, rows_rank, width, channels), frames
+    [k F, (k+1) F) going to rank k (F = frames_per_rank); it receives its own
+    frames' rows from every shard, concatenated in shard order (shard s's
+    chunk: (F, rows_s, width, channels)). Returns (input_splits, output_splits)."""
     rows = [len(shard_row_ids(height, block_rows, n_shards, s)) for s in range(n_shards)]
-    return [rows[rank] * width * channels] * n_shards, [r * width * channels for r in rows]
+    f = frames_per_rank
+    return [f * rows[rank] * width * channels] * n_shards, [f * r * width * channels for r in rows]
+
+
+def assembly_rows(height, block_rows, n_shards, frames):
+    """idx[f * height + r] = row of the received buffer (viewed as rows of
+    width * channels elements: shard chunks (frames, rows_s) in shard order)
+    holding frame f's row r."""
+    base, local, size = np.empty(height, np.int64), np.empty(height, np.int64), []
+    start = 0
+    for s in range(n_shards):
+        ids = shard_row_ids(height, block_rows, n_shards, s)
+        base[ids] = start
+        local[ids] = np.arange(len(ids))
+        size.append(len(ids))
+        start += frames * len(ids)
+    rows_of = np.empty(height, np.int64)
+    for s in range(n_shards):
+        rows_of[shard_row_ids(height, block_rows, n_shards, s)] = size[s]
+    f = np.arange(frames)[:, None]
+    return (base[None, :] + f * rows_of[None, :] + local[None, :]).reshape(-1)
+
+
+def assemble_frames(recv, frames, height, width, block_rows, n_shards, channels=4, idx=None):
+    """recv: this rank's frames' shards as the exchange delivers them (flat;
+    shard s's chunk (frames, rows_s, width, channels), shards in order).
+    Returns (frames, height, width, channels) in row order — one gather."""
+    if idx is None:
+        idx = assembly_rows(height, block_rows, n_shards, frames)
+    flat = recv.reshape(frames * height, width * channels)
+    try:
+        import torch
+        if isinstance(recv, torch.Tensor):
+            i = idx if isinstance(idx, torch.Tensor) else torch.as_tensor(idx, device=recv.device)
+            return flat.index_select(0, i).reshape(frames, height, width, channels)
+    except ImportError:
+        pass
+    return flat[idx].reshape(frames, height, width, channels)
 
 
 def assemble_frame(recv, height, width, block_rows, n_shards, channels=4, perm=None):

@@ -66,34 +66,37 @@ def exchange_worker(rank, world, port, result_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     objs = scenes.bench_objects(16)
-    times = [k / 60.0 for k in range(world)]  # one frame per rank in flight
+    fpr = 2  # frames per rank in flight (bench.py --frames-per-gpu)
+    times = [k / 60.0 for k in range(world * fpr)]
     ids = frame.shard_row_ids(H, BLOCK, world, rank)
     # the batch buffer rt_render_batch writes in bench.py's exchange format
-    # (RT_OUTPUT_RGB32F): (frames, this shard's rows, W, 3)
+    # (RT_OUTPUT_RGB32F): (world * fpr frames, this shard's rows, W, 3)
     data = np.stack([np.concatenate([oracle_port.render(objs, W, H, DEPTH, t, rows=(int(r), int(r) + 1))
                                      for r in ids]) for t in times])[..., :3]
     send = torch.from_numpy(np.ascontiguousarray(data).reshape(-1))
-    in_splits, out_splits = frame.exchange_splits(H, W, BLOCK, world, rank, channels=3)
+    in_splits, out_splits = frame.exchange_splits(H, W, BLOCK, world, rank, channels=3, frames_per_rank=fpr)
     recv = torch.empty(sum(out_splits), dtype=torch.float32)
-    dist.all_to_all_single(recv, send, out_splits, in_splits)  # frame k's rows -> rank k
-    np.save(result_path + ".%d.npy" % rank, frame.assemble_frame(recv, H, W, BLOCK, world, channels=3).numpy())
+    dist.all_to_all_single(recv, send, out_splits, in_splits)  # frames [k fpr, (k+1) fpr) -> rank k
+    np.save(result_path + ".%d.npy" % rank, frame.assemble_frames(recv, fpr, H, W, BLOCK, world, channels=3).numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_exchange_assembles_one_frame_per_rank(tmp_path, world):
-    """bench.py's N-GPU frame exchange: N frames in flight, every rank renders
-    its row blocks of all of them, one all-to-all delivers frame k's rows to
-    rank k, which de-interleaves it — bit-identical to the whole frame's rgb
+    """bench.py's N-GPU frame exchange: 2N frames in flight, every rank renders
+    its row blocks of all of them, one all-to-all delivers frames 2k, 2k+1 to
+    rank k, which de-interleaves them — bit-identical to the whole frame's rgb
     (the shards travel as packed float3; alpha is the constant 0)."""
     from oracle import port as oracle_port, scenes
     out = str(tmp_path / "frame")
     mp.start_processes(exchange_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
     for k in range(world):
-        full = oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, k / 60.0)
-        assert (full[..., 3] == 0).all()
-        assert np.array_equal(np.load(out + ".%d.npy" % k), full[..., :3]), k
+        got = np.load(out + ".%d.npy" % k)
+        for f in range(2):
+            full = oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, (2 * k + f) / 60.0)
+            assert (full[..., 3] == 0).all()
+            assert np.array_equal(got[f], full[..., :3]), (k, f)
 
 
 def mc_worker(rank, world, port, result_path):

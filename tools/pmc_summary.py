@@ -5,7 +5,8 @@ gfx950 corrections of /opt/skills/guides/MI355X_MICROARCH.md (§HBM):
 WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores; FETCH_SIZE
 reports half the bytes of a wide coalesced read, so it is doubled.
 
-usage: python tools/pmc_summary.py gpurun_out/prof/r01 profiles/r01
+usage: python tools/pmc_summary.py gpurun_out/prof/r01 profiles/r01 [FRAMES_PER_LAUNCH]
+(FRAMES_PER_LAUNCH: views per render launch of the profiled bench run, default 8)
 """
 import csv
 import json
@@ -15,6 +16,7 @@ import sys
 from collections import defaultdict
 
 src, dst = sys.argv[1], sys.argv[2]
+frames_per_launch = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 KERNEL = "render_kernel"
 
 
@@ -41,7 +43,8 @@ w, f, sq, cyc = counters("pmc_write"), counters("pmc_fetch"), counters("pmc_sq")
 write_b = mean(w.get("WRITE_SIZE", [])) * 1024 if w.get("WRITE_SIZE") else None
 fetch_b = mean(f.get("FETCH_SIZE", [])) * 1024 * 2 if f.get("FETCH_SIZE") else None
 out = {
-    "workload": "config2", "n_gpus": 1, "kernel": k[0]["Name"] if k else None,
+    "workload": "config2", "n_gpus": 1, "frames_per_launch": frames_per_launch,
+    "kernel": k[0]["Name"] if k else None,
     "avg_kernel_ns": float(k[0]["AverageNs"]) if k else None, "calls": int(k[0]["Calls"]) if k else None,
     "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
     "hbm_bytes_per_launch": (write_b or 0) + (fetch_b or 0) if write_b is not None else None,
