@@ -87,6 +87,9 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.off_lightmat = d.off_lightmat;
     p.off_bvh = d.off_bvh;
     p.off_cone = d.off_cone;
+    p.off_dmask = d.off_dmask;
+    p.dmask_n = d.dmask_n;
+    p.dmask_bytes = d.dmask_bytes;
     p.out_format = ctx->output;
     p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
@@ -362,7 +365,9 @@ bool same_layout(const DeviceScene &a, const DeviceScene &b) {
     return a.blob_units == b.blob_units && a.off_spheres == b.off_spheres && a.off_smeta == b.off_smeta &&
            a.off_boxes == b.off_boxes && a.off_mats == b.off_mats && a.off_lights == b.off_lights &&
            a.off_lightmat == b.off_lightmat && a.off_bvh == b.off_bvh && a.n_bvh == b.n_bvh &&
-           a.off_cone == b.off_cone && a.n_spheres == b.n_spheres && a.n_boxes == b.n_boxes &&
+           a.off_cone == b.off_cone && a.off_dmask == b.off_dmask && a.dmask_n == b.dmask_n &&
+           a.dmask_bytes == b.dmask_bytes &&
+           a.n_spheres == b.n_spheres && a.n_boxes == b.n_boxes &&
            a.n_mats == b.n_mats && a.n_lights == b.n_lights;
 }
 

@@ -42,7 +42,8 @@ struct BoxRec {
     int32_t obj_index;
     int32_t material;
     uint32_t light_inside;  // bit j: light j strictly inside the box with margin (shadow shortcut)
-    int32_t pad[6];
+    int32_t translate_only;  // w2l's 3x3 block is exactly the identity (world->local = + w2l[3,7,11])
+    int32_t pad[5];
 };  // 48 words = 192 B
 static_assert(sizeof(BoxRec) == 192, "BoxRec layout");
 
@@ -76,6 +77,18 @@ struct ShadowCone {
     float sph, cph, near, pad;
 };  // 32 B
 constexpr size_t kConeLdsBudget = 24 * 1024;
+// Shadow-ray direction masks (scenes of at most 32 spheres): for every light
+// that casts shadow rays (not `dead`), a cube map of 6 x n x n texels around
+// the light; texel bit s is set when some direction of the texel lies within
+// sphere s's inflated cone from the light (the ShadowCone geometry, float64,
+// plus the texel's own angular radius and a margin). A shadow ray whose
+// direction from the light falls in the texel can only be blocked by the
+// spheres of its mask. Face f = 2 * axis + (component < 0); within the face
+// the two other axes in increasing order give (column, row). Kept while the
+// work-group's LDS stays within kMaskLdsBudget (full occupancy); scenes of
+// at most 16 spheres store 16-bit masks, which buys finer texels.
+constexpr int kMaskMaxSpheres = 32;
+constexpr size_t kMaskLdsBudget = 19 * 1024;
 // Sphere BVH node (depth-first order; the left child is the next node):
 // lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
 // this subtree (-1: end) and leaf = (count << 24) | first sphere slot (0 for
@@ -124,6 +137,8 @@ struct LaunchParams {
     int32_t off_bvh, n_bvh;  // sphere BVH nodes (2 x float4 each), 16-B units / count
     int32_t off_cone;        // n_lights x n_spheres ShadowCone, 16-B units; -1: none
                              // (kept only while the LDS total stays within kConeLdsBudget)
+    int32_t off_dmask, dmask_n;  // shadow direction masks (live lights x 6 x n x n), 16-B units; -1: none
+    int32_t dmask_bytes;         // bytes per mask: 2 (at most 16 spheres) or 4
     int32_t blob_units;      // blob size, 16-B units
     // Monte-Carlo accumulation (render_kernel<D, true>): samples
     // [sample0, sample0 + spp) per pixel, jittered inside the pixel when
@@ -158,6 +173,7 @@ struct DeviceScene {
     int32_t blob_units = 0;
     int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
     int32_t off_bvh = 0, n_bvh = 0, off_cone = 0;
+    int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
 

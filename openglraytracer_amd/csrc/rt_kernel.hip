@@ -222,6 +222,8 @@ struct Scene {
     const LightMatRec *lm;
     const float4 *bvh;  // BvhNode pairs (lo, hi)
     const ShadowCone *cone;  // [light][sphere] shadow culling cones
+    const char *dmask;  // [live light][face][row][col] shadow direction masks (nullptr: none)
+    int dmask_n, dmask_bytes;
     // The same box and light records in the device blob through the constant
     // address space: a wave-uniform record index becomes scalar loads into
     // SGPRs (no LDS round trip, no VGPRs) — used where the index is uniform.
@@ -325,6 +327,14 @@ __device__ __forceinline__ bool quotient_below_one(float num, float d) {
 // light is inside the box with a margin (host, float64), so a segment that
 // starts inside ends inside too and exits past t = 1.
 __device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, uint32_t light_bit) {
+    if ((b.light_inside & light_bit) && b.translate_only) {
+        // identity rotation: xform_point is ((1 x + 0 y) + 0 z) + w, which for
+        // finite start equals x + w up to the sign of a zero (comparisons
+        // alike); a non-finite component stays non-finite here and fails
+        // strictly_inside, so a pass implies the full transform passes too
+        const v3 rq = mk(start.x + b.w2l[3], start.y + b.w2l[7], start.z + b.w2l[11]);
+        if (strictly_inside(b, rq)) return false;
+    }
     const v3 rs = xform_point(b.w2l, start);
     const bool inside = strictly_inside(b, rs);
     if (inside && (b.light_inside & light_bit)) return false;
@@ -511,20 +521,48 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
     return h;
 }
 
+// Mask of the texel of direction u in a light's cube map (rt_internal.h,
+// kMaskMaxSpheres): face = the largest |component| (ties to the lower axis),
+// column / row from the other two components over it. Approximate
+// arithmetic: the host's texel cones carry a margin far above its error. A
+// direction without a usable largest component gets every sphere.
+__device__ __forceinline__ uint32_t direction_mask(const void *tab, int n, int bytes, v3 u, int ns) {
+    const float ax = fabsf(u.x), ay = fabsf(u.y), az = fabsf(u.z);
+    const bool fx = ax >= ay && ax >= az, fy = !fx && ay >= az;
+    const float um = fx ? u.x : (fy ? u.y : u.z);
+    const float ua = fx ? u.y : u.x, ub = fy || fx ? u.z : u.y;
+    const int face = 2 * (fx ? 0 : (fy ? 1 : 2)) + (um < 0.0f ? 1 : 0);
+    const float am = fabsf(um);
+    const uint32_t all = ns >= 32 ? 0xFFFFFFFFu : (1u << ns) - 1u;
+    if (!(am > 1e-20f && am < 1e30f)) return all;
+    const float h = 0.5f * static_cast<float>(n) * __builtin_amdgcn_rcpf(am);
+    const int col = min(max(static_cast<int>(floorf(ua * h + 0.5f * n)), 0), n - 1);
+    const int row = min(max(static_cast<int>(floorf(ub * h + 0.5f * n)), 0), n - 1);
+    const int at = (face * n + row) * n + col;
+    return bytes == 2 ? static_cast<const uint16_t *>(tab)[at] : static_cast<const uint32_t *>(tab)[at];
+}
+
 // Shadow query (:807-819) for the lanes with `need`: is there an object with
 // 0 < t < 1 along start + t * dir? (equivalent to the closest hit's t < 1).
 // p = the shaded point, L = the light. Called with all lanes active.
-__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, bool need) {
+__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
+                                         bool need) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     for (int b = 0; b < S.nb; ++b)
         if (need && !hit) hit = box_occludes(cload(S.cbox + b), start, dir, light_bit);
     if (!__any(need && !hit)) return hit;
+#ifdef RT_ABLATE_SPHSHADOW
+    return hit;
+#endif
     const v3 d2 = muls(dir, 2.0f);
     const float qa = dot(dir, dir);
     const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
     const float floor = root_floor(qa2);
     auto exact = [&](int s) {
+#ifdef RT_ABLATE_EXACT
+        if (s < 0)
+#endif
         if (need && !hit) {
             const float4 c = S.sph[s];
             const v3 oc = sub(start, mk(c.x, c.y, c.z));
@@ -537,6 +575,21 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         for (int s = 0; s < S.ns; ++s) {
             if (!__any(need && !hit)) break;
             exact(s);
+        }
+        return hit;
+    }
+    if (S.dmask) {
+        // the spheres that may block this lane's ray: the mask of the texel
+        // its direction from the light (p - L = -dir) falls in; each lane
+        // walks its own mask (usually empty)
+        const int table = slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes;
+        uint32_t cand = need && !hit ? direction_mask(S.dmask + table, S.dmask_n, S.dmask_bytes, muls(dir, -1.0f), S.ns)
+                                     : 0u;
+        while (__any(cand != 0u)) {
+            if (cand) {
+                exact(__builtin_ctz(cand));
+                cand = hit ? 0u : cand & (cand - 1u);
+            }
         }
         return hit;
     }
@@ -715,9 +768,11 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
     const MatRec &m = S.mat[c.material];
     float4 dif = make_float4(0.0f, 0.0f, 0.0f, 0.0f), spe = dif;
     const v3 view = normalize(muls(r.dir, -1.0f));
+    int slot = -1;  // index among the live lights (direction masks)
     for (int j = 0; j < S.nl; ++j) {
         const LightRec L = cload(S.clight + j);
         if (L.dead != 0.0f) continue;  // no direct term for any material (host-checked)
+        ++slot;
         const v3 lpos = mk(L.pos[0], L.pos[1], L.pos[2]);
         const v3 ldir = normalize(sub(lpos, c.p));
         const v3 lref = normalize(reflect(muls(ldir, -1.0f), c.n));
@@ -730,7 +785,11 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         const float xs = gmax(cos_phi, 0.0f);
         const bool need_pow = !(xs == 0.0f && m.shininess > 0.0f);
         float ks = 0.0f;
+#ifdef RT_ABLATE_POW
+        ks = xs;
+#else
         if (__any(need_pow && valid)) ks = need_pow ? glsl_pow(xs, m.shininess) : 0.0f;
+#endif
         const float4 nd = make_float4(dif.x + q.ld_md[0] * kd, dif.y + q.ld_md[1] * kd, dif.z + q.ld_md[2] * kd,
                                       dif.w + q.ld_md[3] * kd);
         const float4 ns = make_float4(spe.x + q.ls_ms[0] * ks, spe.y + q.ls_ms[1] * ks, spe.z + q.ls_ms[2] * ks,
@@ -746,7 +805,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         continue;
 #endif
         if (__any(need)) {
-            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sub(lpos, c.p), c.p, lpos, j, need);
+            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sub(lpos, c.p), c.p, lpos, j, slot, need);
             if (need && !shadowed) {
                 dif = nd;
                 spe = ns;
@@ -1199,6 +1258,9 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
     S.bvh = lds + p.off_bvh;
     S.cone = p.off_cone >= 0 ? reinterpret_cast<const ShadowCone *>(lds + p.off_cone) : nullptr;
+    S.dmask = p.off_dmask >= 0 ? reinterpret_cast<const char *>(lds + p.off_dmask) : nullptr;
+    S.dmask_n = p.dmask_n;
+    S.dmask_bytes = p.dmask_bytes;
     S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
     S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
     S.nbvh = p.n_bvh;

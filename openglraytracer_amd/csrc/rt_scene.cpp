@@ -494,6 +494,76 @@ static void view_frame_setup(const LaunchParams &p, const FrameView &V, const fl
 
 // Build the device blob: [spheres][sphere meta][boxes][materials][lights]
 // [light x material products]; every section 16-B aligned.
+// Shadow direction masks (rt_internal.h, kMaskMaxSpheres): float64 geometry.
+// A shadow ray from shaded point p runs from p + 0.01 n towards the light L
+// (:808-809): within 0.01 of the segment [L, p], i.e. of the ray from L in
+// the direction of p - L. Sphere s (centre c, radius r, d = |c - L|) can
+// block it only if that ray passes within rp = r + 0.021 + 1e-3 d of c (the
+// ShadowCone inflation): its direction within asin(rp / d) of (c - L) / d,
+// or any direction when d <= rp. A texel is the spherical image of a square
+// of the cube face; it lies inside the cone around its centre direction
+// whose half-angle is the largest angle to its four corners (a cone narrower
+// than 90 degrees is convex, so holding the corners it holds the square).
+static void build_direction_masks(const std::vector<SphereRec> &sph, const std::vector<SphereMeta> &smeta,
+                           const rt_light *lights, const std::vector<LightRec> &lrec, int n,
+                           std::vector<uint32_t> &out) {
+    const int n_lights = static_cast<int>(lrec.size());
+    out.clear();
+    auto unit = [](double v[3]) {
+        const double l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        for (int k = 0; k < 3; ++k) v[k] /= l;
+    };
+    auto angle = [](const double a[3], const double b[3]) {
+        const double c = a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+        return std::acos(std::max(-1.0, std::min(1.0, c)));
+    };
+    for (int j = 0; j < n_lights; ++j) {
+        if (lrec[j].dead != 0.0f) continue;
+        // each sphere's cone from this light: axis, half-angle (or everywhere)
+        std::vector<double> ax(3 * sph.size()), half(sph.size());
+        std::vector<char> every(sph.size(), 0);
+        for (size_t s = 0; s < sph.size(); ++s) {
+            double v[3] = {double(sph[s].cx) - lights[j].position[0], double(sph[s].cy) - lights[j].position[1],
+                           double(sph[s].cz) - lights[j].position[2]};
+            const double d = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+            const double rp = double(smeta[s].radius) + 0.021 + 1e-3 * d;
+            if (!(std::isfinite(d) && std::isfinite(rp)) || d <= rp) {
+                every[s] = 1;
+                continue;
+            }
+            for (int k = 0; k < 3; ++k) ax[3 * s + k] = v[k] / d;
+            half[s] = std::asin(std::min(1.0, rp / d));
+        }
+        for (int f = 0; f < 6; ++f) {
+            const int m = f >> 1, a = m == 0 ? 1 : 0, b = m == 2 ? 1 : 2;
+            const double sg = (f & 1) ? -1.0 : 1.0;
+            for (int row = 0; row < n; ++row)
+                for (int col = 0; col < n; ++col) {
+                    const double a0 = -1.0 + 2.0 * col / n, a1 = -1.0 + 2.0 * (col + 1) / n;
+                    const double b0 = -1.0 + 2.0 * row / n, b1 = -1.0 + 2.0 * (row + 1) / n;
+                    double w[3];
+                    w[m] = sg;
+                    w[a] = 0.5 * (a0 + a1);
+                    w[b] = 0.5 * (b0 + b1);
+                    unit(w);
+                    double alpha = 0.0;
+                    for (int k = 0; k < 4; ++k) {
+                        double q[3];
+                        q[m] = sg;
+                        q[a] = (k & 1) ? a1 : a0;
+                        q[b] = (k & 2) ? b1 : b0;
+                        unit(q);
+                        alpha = std::max(alpha, angle(w, q));
+                    }
+                    uint32_t bits = 0;
+                    for (size_t s = 0; s < sph.size(); ++s)
+                        if (every[s] || angle(w, &ax[3 * s]) <= alpha + half[s] + 1e-3) bits |= 1u << s;
+                    out.push_back(bits);
+                }
+        }
+    }
+}
+
 int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
                 int n_lights, std::vector<float4> &blob, DeviceScene &ds) {
     std::vector<SphereRec> sph;
@@ -529,6 +599,10 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             std::memcpy(b.maxs, o.box_maxs, 12);
             b.obj_index = i;
             b.material = o.material;
+            b.translate_only = 1;
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c)
+                    if (b.w2l[r * 4 + c] != (r == c ? 1.0f : 0.0f)) b.translate_only = 0;
             // Lights strictly inside the box by a margin (float64): a shadow
             // segment that starts inside the box then ends inside it too (its
             // end is the light + 0.01 n, :808-809), so the box cannot occlude.
@@ -635,8 +709,39 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     // 24 KB and cut the resident work-groups per CU); without it the kernel
     // derives the cones per wave (off_cone = -1).
     const size_t per_frame = sph.size() * 32 + boxes.size() * 16;
+    // Direction masks replace the cone table where they fit (finest texels first).
+    int n_live = 0;
+    for (int j = 0; j < n_lights; ++j) n_live += lrec[j].dead == 0.0f;
+    std::vector<uint32_t> dmask;
+    ds.off_dmask = -1;
+    ds.dmask_n = 0;
+    if (!sph.empty() && sph.size() <= static_cast<size_t>(kMaskMaxSpheres) && n_live > 0) {
+        ds.dmask_bytes = sph.size() <= 16 ? 2 : 4;
+#ifndef RT_DMASK_MAXN
+#define RT_DMASK_MAXN 12
+#endif
+        for (int n : {32, 24, 16, 12, 8}) {
+            if (n > RT_DMASK_MAXN) continue;
+            const size_t bytes = static_cast<size_t>(n_live) * 6 * n * n * ds.dmask_bytes;
+            if ((static_cast<size_t>(off) + units(bytes)) * 16 + per_frame <= kMaskLdsBudget) {
+                ds.dmask_n = n;
+                break;
+            }
+        }
+    }
+    if (ds.dmask_n > 0) {
+        build_direction_masks(sph, smeta, lights, lrec, ds.dmask_n, dmask);
+        ds.off_dmask = off;
+        if (ds.dmask_bytes == 2) {  // 16-bit masks, packed in place
+            std::vector<uint16_t> narrow(dmask.begin(), dmask.end());
+            dmask.assign((narrow.size() + 1) / 2, 0u);
+            std::memcpy(dmask.data(), narrow.data(), narrow.size() * 2);
+        }
+        off += units(dmask.size() * 4);
+        cones.clear();
+    }
     const size_t with_cones = (static_cast<size_t>(off) + units(cones.size() * sizeof(ShadowCone))) * 16 + per_frame;
-    if (with_cones <= kConeLdsBudget) {
+    if (ds.dmask_n == 0 && with_cones <= kConeLdsBudget) {
         ds.off_cone = off;
         off += units(cones.size() * sizeof(ShadowCone));
     } else {
@@ -661,6 +766,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     put(ds.off_lightmat, lm.data(), lm.size() * sizeof(LightMatRec));
     put(ds.off_bvh, bvh.data(), bvh.size() * sizeof(BvhNode));
     if (ds.off_cone >= 0) put(ds.off_cone, cones.data(), cones.size() * sizeof(ShadowCone));
+    if (ds.off_dmask >= 0) put(ds.off_dmask, dmask.data(), dmask.size() * 4);
     return RT_OK;
 }
 
