@@ -545,7 +545,7 @@ __device__ __forceinline__ uint32_t direction_mask(const void *tab, int n, int b
 // Shadow query (:807-819) for the lanes with `need`: is there an object with
 // 0 < t < 1 along start + t * dir? (equivalent to the closest hit's t < 1).
 // p = the shaded point, L = the light. Called with all lanes active.
-__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
+__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, uint32_t mask,
                                          bool need) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
@@ -579,12 +579,10 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         return hit;
     }
     if (S.dmask) {
-        // the spheres that may block this lane's ray: the mask of the texel
-        // its direction from the light (p - L = -dir) falls in; each lane
-        // walks its own mask (usually empty)
-        const int table = slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes;
-        uint32_t cand = need && !hit ? direction_mask(S.dmask + table, S.dmask_n, S.dmask_bytes, muls(dir, -1.0f), S.ns)
-                                     : 0u;
+        // the spheres that may block this lane's ray: `mask`, the texel mask
+        // of its direction from the light (looked up by the caller); each
+        // lane walks its own mask (usually empty)
+        uint32_t cand = need && !hit ? mask : 0u;
         while (__any(cand != 0u)) {
             if (cand) {
                 exact(__builtin_ctz(cand));
@@ -774,7 +772,14 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         if (L.dead != 0.0f) continue;  // no direct term for any material (host-checked)
         ++slot;
         const v3 lpos = mk(L.pos[0], L.pos[1], L.pos[2]);
-        const v3 ldir = normalize(sub(lpos, c.p));
+        const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
+        // its direction-mask texel, looked up ahead of the shading math so
+        // the LDS read overlaps it (p - L = -sdir)
+        const uint32_t smask =
+            S.dmask && valid ? direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
+                                              S.dmask_bytes, muls(sdir, -1.0f), S.ns)
+                             : 0u;
+        const v3 ldir = normalize(sdir);
         const v3 lref = normalize(reflect(muls(ldir, -1.0f), c.n));
         const float cos_theta = dot(ldir, c.n);
         const float cos_phi = dot(view, lref);
@@ -805,7 +810,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         continue;
 #endif
         if (__any(need)) {
-            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sub(lpos, c.p), c.p, lpos, j, slot, need);
+            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, smask, need);
             if (need && !shadowed) {
                 dif = nd;
                 spe = ns;

@@ -526,3 +526,41 @@ def test_animated_frames_in_one_launch(gpu_ctx):
     assert e.value.code == rt.abi.RT_ERR_INVALID
     for s in scs + [other]:
         s.close()
+
+
+@pytest.mark.parametrize("n_spheres", [3, 16, 17, 32, 33])
+def test_shadow_direction_masks(gpu_ctx, n_spheres):
+    """Shadow-ray direction masks (rt_internal.h, kMaskMaxSpheres): 16-bit
+    masks up to 16 spheres, 32-bit up to 32, the per-wave cone above. Spheres
+    cluster around the lights (one light inside a sphere, one grazing a
+    surface) so that many shadow rays are blocked; culling on and off and the
+    oracle must agree bit for bit, at depth 0 and through reflections."""
+    rng = np.random.default_rng(n_spheres)
+    lights = rt.reference_lights()
+    lights[1].position[:] = (2.0, 2.0, 1.0)
+    lights[2].position[:] = (-3.0, 1.0, -2.0)
+    extra = rt.reference_lights()[1]
+    extra.position[:] = (0.5, -4.0, 3.0)
+    lights = lights + [extra]
+    objs = [scenes.room_box(), scenes.sphere((2.0, 2.0, 1.0), 0.6, rt.abi.RED_GLASS),
+            scenes.sphere((-3.0, 1.0, -2.75), 0.7, rt.abi.MATERIAL1)]  # light 2 ~0.05 above its top
+    mats_cycle = [rt.abi.MATERIAL1, rt.abi.MATERIAL2, rt.abi.MIRROR, rt.abi.GREEN_GLASS, rt.abi.BLUE_GLASS]
+    for i in range(n_spheres - 2):
+        anchor = np.array(lights[1 + i % 3].position[:])
+        c = anchor + rng.uniform(-4.0, 4.0, 3)
+        objs.append(scenes.sphere(tuple(float(v) for v in c), float(rng.uniform(0.2, 0.9)), mats_cycle[i % 5]))
+    objs = objs[:n_spheres + 1]
+    view = rt.make_view(None, 0.0)
+    for depth in (0, 2):
+        sc = rt.Scene(gpu_ctx, objs, lights=lights)
+        try:
+            gpu_ctx.set_culling(True)
+            on = rt.render(gpu_ctx, sc, 128, 72, depth, view=view)
+            gpu_ctx.set_culling(False)
+            off = rt.render(gpu_ctx, sc, 128, 72, depth, view=view)
+        finally:
+            gpu_ctx.set_culling(True)
+            sc.close()
+        assert np.array_equal(on, off, equal_nan=True), (depth, parity_stats(on, off))
+        o = oracle_render(objs, 128, 72, depth, lights=lights)
+        assert np.array_equal(on, o, equal_nan=True), (depth, parity_stats(on, o))
