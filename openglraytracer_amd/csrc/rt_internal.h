@@ -77,7 +77,7 @@ struct ShadowCone {
     float sph, cph, near, pad;
 };  // 32 B
 constexpr size_t kConeLdsBudget = 24 * 1024;
-// Shadow-ray direction masks (scenes of at most 32 spheres): for every light
+// Shadow-ray direction masks (scenes of at most 64 spheres): for every light
 // that casts shadow rays (not `dead`), a cube map of 6 x n x n texels around
 // the light; texel bit s is set when some direction of the texel lies within
 // sphere s's inflated cone from the light (the ShadowCone geometry, float64,
@@ -85,9 +85,9 @@ constexpr size_t kConeLdsBudget = 24 * 1024;
 // direction from the light falls in the texel can only be blocked by the
 // spheres of its mask. Face f = 2 * axis + (component < 0); within the face
 // the two other axes in increasing order give (column, row). Kept while the
-// work-group's LDS stays within kMaskLdsBudget (full occupancy); scenes of
-// at most 16 spheres store 16-bit masks, which buys finer texels.
-constexpr int kMaskMaxSpheres = 32;
+// work-group's LDS stays within kMaskLdsBudget (full occupancy); masks are
+// 16, 32 or 64 bits wide (scenes of at most 16, 32, 64 spheres).
+constexpr int kMaskMaxSpheres = 64;
 constexpr size_t kMaskLdsBudget = 19 * 1024;
 // Sphere BVH node (depth-first order; the left child is the next node):
 // lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
@@ -138,7 +138,7 @@ struct LaunchParams {
     int32_t off_cone;        // n_lights x n_spheres ShadowCone, 16-B units; -1: none
                              // (kept only while the LDS total stays within kConeLdsBudget)
     int32_t off_dmask, dmask_n;  // shadow direction masks (live lights x 6 x n x n), 16-B units; -1: none
-    int32_t dmask_bytes;         // bytes per mask: 2 (at most 16 spheres) or 4
+    int32_t dmask_bytes;         // bytes per mask: 2, 4 or 8 (at most 16, 32, 64 spheres)
     int32_t blob_units;      // blob size, 16-B units
     // Monte-Carlo accumulation (render_kernel<D, true>): samples
     // [sample0, sample0 + spp) per pixel, jittered inside the pixel when

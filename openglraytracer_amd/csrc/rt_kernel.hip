@@ -526,26 +526,27 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
 // column / row from the other two components over it. Approximate
 // arithmetic: the host's texel cones carry a margin far above its error. A
 // direction without a usable largest component gets every sphere.
-__device__ __forceinline__ uint32_t direction_mask(const void *tab, int n, int bytes, v3 u, int ns) {
+__device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int bytes, v3 u, int ns) {
     const float ax = fabsf(u.x), ay = fabsf(u.y), az = fabsf(u.z);
     const bool fx = ax >= ay && ax >= az, fy = !fx && ay >= az;
     const float um = fx ? u.x : (fy ? u.y : u.z);
     const float ua = fx ? u.y : u.x, ub = fy || fx ? u.z : u.y;
     const int face = 2 * (fx ? 0 : (fy ? 1 : 2)) + (um < 0.0f ? 1 : 0);
     const float am = fabsf(um);
-    const uint32_t all = ns >= 32 ? 0xFFFFFFFFu : (1u << ns) - 1u;
+    const uint64_t all = ns >= 64 ? ~uint64_t{0} : (uint64_t{1} << ns) - 1u;
     if (!(am > 1e-20f && am < 1e30f)) return all;
     const float h = 0.5f * static_cast<float>(n) * __builtin_amdgcn_rcpf(am);
     const int col = min(max(static_cast<int>(floorf(ua * h + 0.5f * n)), 0), n - 1);
     const int row = min(max(static_cast<int>(floorf(ub * h + 0.5f * n)), 0), n - 1);
     const int at = (face * n + row) * n + col;
+    if (bytes == 8) return static_cast<const uint64_t *>(tab)[at];
     return bytes == 2 ? static_cast<const uint16_t *>(tab)[at] : static_cast<const uint32_t *>(tab)[at];
 }
 
 // Shadow query (:807-819) for the lanes with `need`: is there an object with
 // 0 < t < 1 along start + t * dir? (equivalent to the closest hit's t < 1).
 // p = the shaded point, L = the light. Called with all lanes active.
-__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, uint32_t mask,
+__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, uint64_t mask,
                                          bool need) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
@@ -582,11 +583,21 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         // the spheres that may block this lane's ray: `mask`, the texel mask
         // of its direction from the light (looked up by the caller); each
         // lane walks its own mask (usually empty)
-        uint32_t cand = need && !hit ? mask : 0u;
-        while (__any(cand != 0u)) {
-            if (cand) {
-                exact(__builtin_ctz(cand));
-                cand = hit ? 0u : cand & (cand - 1u);
+        if (S.dmask_bytes == 8) {
+            uint64_t cand = need && !hit ? mask : 0u;
+            while (__any(cand != 0u)) {
+                if (cand) {
+                    exact(__builtin_ctzll(cand));
+                    cand = hit ? 0u : cand & (cand - 1u);
+                }
+            }
+        } else {  // 32-bit masks: half the bit arithmetic
+            uint32_t cand = need && !hit ? static_cast<uint32_t>(mask) : 0u;
+            while (__any(cand != 0u)) {
+                if (cand) {
+                    exact(__builtin_ctz(cand));
+                    cand = hit ? 0u : cand & (cand - 1u);
+                }
             }
         }
         return hit;
@@ -775,7 +786,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
         // its direction-mask texel, looked up ahead of the shading math so
         // the LDS read overlaps it (p - L = -sdir)
-        const uint32_t smask =
+        const uint64_t smask =
             S.dmask && valid ? direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
                                               S.dmask_bytes, muls(sdir, -1.0f), S.ns)
                              : 0u;

@@ -506,7 +506,7 @@ static void view_frame_setup(const LaunchParams &p, const FrameView &V, const fl
 // than 90 degrees is convex, so holding the corners it holds the square).
 static void build_direction_masks(const std::vector<SphereRec> &sph, const std::vector<SphereMeta> &smeta,
                            const rt_light *lights, const std::vector<LightRec> &lrec, int n,
-                           std::vector<uint32_t> &out) {
+                           std::vector<uint64_t> &out) {
     const int n_lights = static_cast<int>(lrec.size());
     out.clear();
     auto unit = [](double v[3]) {
@@ -555,9 +555,9 @@ static void build_direction_masks(const std::vector<SphereRec> &sph, const std::
                         unit(q);
                         alpha = std::max(alpha, angle(w, q));
                     }
-                    uint32_t bits = 0;
+                    uint64_t bits = 0;
                     for (size_t s = 0; s < sph.size(); ++s)
-                        if (every[s] || angle(w, &ax[3 * s]) <= alpha + half[s] + 1e-3) bits |= 1u << s;
+                        if (every[s] || angle(w, &ax[3 * s]) <= alpha + half[s] + 1e-3) bits |= uint64_t{1} << s;
                     out.push_back(bits);
                 }
         }
@@ -712,11 +712,11 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     // Direction masks replace the cone table where they fit (finest texels first).
     int n_live = 0;
     for (int j = 0; j < n_lights; ++j) n_live += lrec[j].dead == 0.0f;
-    std::vector<uint32_t> dmask;
+    std::vector<uint64_t> dmask;
     ds.off_dmask = -1;
     ds.dmask_n = 0;
     if (!sph.empty() && sph.size() <= static_cast<size_t>(kMaskMaxSpheres) && n_live > 0) {
-        ds.dmask_bytes = sph.size() <= 16 ? 2 : 4;
+        ds.dmask_bytes = sph.size() <= 16 ? 2 : (sph.size() <= 32 ? 4 : 8);
 #ifndef RT_DMASK_MAXN
 #define RT_DMASK_MAXN 12
 #endif
@@ -729,15 +729,14 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             }
         }
     }
+    std::vector<char> dmask_bytes;
     if (ds.dmask_n > 0) {
         build_direction_masks(sph, smeta, lights, lrec, ds.dmask_n, dmask);
         ds.off_dmask = off;
-        if (ds.dmask_bytes == 2) {  // 16-bit masks, packed in place
-            std::vector<uint16_t> narrow(dmask.begin(), dmask.end());
-            dmask.assign((narrow.size() + 1) / 2, 0u);
-            std::memcpy(dmask.data(), narrow.data(), narrow.size() * 2);
-        }
-        off += units(dmask.size() * 4);
+        dmask_bytes.resize(dmask.size() * ds.dmask_bytes);
+        for (size_t i = 0; i < dmask.size(); ++i)  // little-endian: the low bytes of each mask
+            std::memcpy(dmask_bytes.data() + i * ds.dmask_bytes, &dmask[i], ds.dmask_bytes);
+        off += units(dmask_bytes.size());
         cones.clear();
     }
     const size_t with_cones = (static_cast<size_t>(off) + units(cones.size() * sizeof(ShadowCone))) * 16 + per_frame;
@@ -766,7 +765,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     put(ds.off_lightmat, lm.data(), lm.size() * sizeof(LightMatRec));
     put(ds.off_bvh, bvh.data(), bvh.size() * sizeof(BvhNode));
     if (ds.off_cone >= 0) put(ds.off_cone, cones.data(), cones.size() * sizeof(ShadowCone));
-    if (ds.off_dmask >= 0) put(ds.off_dmask, dmask.data(), dmask.size() * 4);
+    if (ds.off_dmask >= 0) put(ds.off_dmask, dmask_bytes.data(), dmask_bytes.size());
     return RT_OK;
 }
 
