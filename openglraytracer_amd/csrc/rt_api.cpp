@@ -90,6 +90,8 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
     p.off_dmask = d.off_dmask;
     p.dmask_n = d.dmask_n;
     p.dmask_bytes = d.dmask_bytes;
+    p.off_gmask = d.off_gmask;
+    p.gmask_words = d.gmask_words;
     p.out_format = ctx->output;
     p.n_bvh = d.n_bvh;
     p.blob_units = d.blob_units;
@@ -207,7 +209,7 @@ int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt
     s->device = ctx->device;
     s->dev = ds;
     s->host.swap(blob);
-    s->capacity_units = ds.blob_units > 0 ? ds.blob_units : 1;
+    s->capacity_units = static_cast<int32_t>(s->host.size());
     *out = s;
     return RT_OK;
 }
@@ -237,13 +239,13 @@ int rt_scene_update(rt_context *ctx, rt_scene *scene, const rt_object *objs, int
     // renders already queued on the context's stream may still read the blob
     e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
-    if (ds.blob_units > scene->capacity_units) {
+    if (static_cast<int32_t>(blob.size()) > scene->capacity_units) {
         void *nb = nullptr;
         e = hipMalloc(&nb, blob.size() * sizeof(float4));
         if (e != hipSuccess) return hip_fail("hipMalloc(scene)", e);
         (void)hipFree(scene->dev.blob);
         scene->dev.blob = nb;
-        scene->capacity_units = ds.blob_units;
+        scene->capacity_units = static_cast<int32_t>(blob.size());
     }
     e = hipMemcpy(scene->dev.blob, blob.data(), blob.size() * sizeof(float4), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail("hipMemcpy(scene)", e);
@@ -366,7 +368,7 @@ bool same_layout(const DeviceScene &a, const DeviceScene &b) {
            a.off_boxes == b.off_boxes && a.off_mats == b.off_mats && a.off_lights == b.off_lights &&
            a.off_lightmat == b.off_lightmat && a.off_bvh == b.off_bvh && a.n_bvh == b.n_bvh &&
            a.off_cone == b.off_cone && a.off_dmask == b.off_dmask && a.dmask_n == b.dmask_n &&
-           a.dmask_bytes == b.dmask_bytes &&
+           a.dmask_bytes == b.dmask_bytes && a.off_gmask == b.off_gmask && a.gmask_words == b.gmask_words &&
            a.n_spheres == b.n_spheres && a.n_boxes == b.n_boxes &&
            a.n_mats == b.n_mats && a.n_lights == b.n_lights;
 }

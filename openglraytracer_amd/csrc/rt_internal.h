@@ -89,6 +89,11 @@ constexpr size_t kConeLdsBudget = 24 * 1024;
 // 16, 32 or 64 bits wide (scenes of at most 16, 32, 64 spheres).
 constexpr int kMaskMaxSpheres = 64;
 constexpr size_t kMaskLdsBudget = 19 * 1024;
+// Larger scenes (up to kGMaskMaxSpheres) use the same masks as 64-bit words
+// per texel, kGMaskTexels per face edge, in the device blob after the part
+// the work-groups stage (read through L2: config 4, 256 spheres, 2 x 96 KB).
+constexpr int kGMaskMaxSpheres = 256;
+constexpr int kGMaskTexels = 16;
 // Sphere BVH node (depth-first order; the left child is the next node):
 // lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
 // this subtree (-1: end) and leaf = (count << 24) | first sphere slot (0 for
@@ -139,6 +144,7 @@ struct LaunchParams {
                              // (kept only while the LDS total stays within kConeLdsBudget)
     int32_t off_dmask, dmask_n;  // shadow direction masks (live lights x 6 x n x n), 16-B units; -1: none
     int32_t dmask_bytes;         // bytes per mask: 2, 4 or 8 (at most 16, 32, 64 spheres)
+    int32_t off_gmask, gmask_words;  // wide masks in the blob past blob_units (not staged), 16-B units; -1: none
     int32_t blob_units;      // blob size, 16-B units
     // Monte-Carlo accumulation (render_kernel<D, true>): samples
     // [sample0, sample0 + spp) per pixel, jittered inside the pixel when
@@ -174,6 +180,7 @@ struct DeviceScene {
     int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
     int32_t off_bvh = 0, n_bvh = 0, off_cone = 0;
     int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
+    int32_t off_gmask = -1, gmask_words = 0;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
 

@@ -224,6 +224,8 @@ struct Scene {
     const ShadowCone *cone;  // [light][sphere] shadow culling cones
     const char *dmask;  // [live light][face][row][col] shadow direction masks (nullptr: none)
     int dmask_n, dmask_bytes;
+    const uint64_t *gmask;  // wide masks in global memory: [live light][texel][word] (nullptr: none)
+    int gwords;
     // The same box and light records in the device blob through the constant
     // address space: a wave-uniform record index becomes scalar loads into
     // SGPRs (no LDS round trip, no VGPRs) — used where the index is uniform.
@@ -526,19 +528,23 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
 // column / row from the other two components over it. Approximate
 // arithmetic: the host's texel cones carry a margin far above its error. A
 // direction without a usable largest component gets every sphere.
-__device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int bytes, v3 u, int ns) {
+// Texel of direction u, or -1.
+__device__ __forceinline__ int direction_texel(int n, v3 u) {
     const float ax = fabsf(u.x), ay = fabsf(u.y), az = fabsf(u.z);
     const bool fx = ax >= ay && ax >= az, fy = !fx && ay >= az;
     const float um = fx ? u.x : (fy ? u.y : u.z);
     const float ua = fx ? u.y : u.x, ub = fy || fx ? u.z : u.y;
     const int face = 2 * (fx ? 0 : (fy ? 1 : 2)) + (um < 0.0f ? 1 : 0);
     const float am = fabsf(um);
-    const uint64_t all = ns >= 64 ? ~uint64_t{0} : (uint64_t{1} << ns) - 1u;
-    if (!(am > 1e-20f && am < 1e30f)) return all;
+    if (!(am > 1e-20f && am < 1e30f)) return -1;
     const float h = 0.5f * static_cast<float>(n) * __builtin_amdgcn_rcpf(am);
     const int col = min(max(static_cast<int>(floorf(ua * h + 0.5f * n)), 0), n - 1);
     const int row = min(max(static_cast<int>(floorf(ub * h + 0.5f * n)), 0), n - 1);
-    const int at = (face * n + row) * n + col;
+    return (face * n + row) * n + col;
+}
+__device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int bytes, v3 u, int ns) {
+    const int at = direction_texel(n, u);
+    if (at < 0) return ns >= 64 ? ~uint64_t{0} : (uint64_t{1} << ns) - 1u;
     if (bytes == 8) return static_cast<const uint64_t *>(tab)[at];
     return bytes == 2 ? static_cast<const uint16_t *>(tab)[at] : static_cast<const uint32_t *>(tab)[at];
 }
@@ -546,8 +552,8 @@ __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int b
 // Shadow query (:807-819) for the lanes with `need`: is there an object with
 // 0 < t < 1 along start + t * dir? (equivalent to the closest hit's t < 1).
 // p = the shaded point, L = the light. Called with all lanes active.
-__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, uint64_t mask,
-                                         bool need) {
+__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
+                                         uint64_t mask, bool need) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     for (int b = 0; b < S.nb; ++b)
@@ -576,6 +582,28 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         for (int s = 0; s < S.ns; ++s) {
             if (!__any(need && !hit)) break;
             exact(s);
+        }
+        return hit;
+    }
+    if (S.gmask) {
+        // wide masks from L2: `mask` holds the texel (-1: every sphere); the
+        // words are read one at a time, each walked like the LDS masks below
+        const int texel = static_cast<int>(static_cast<int64_t>(mask));
+        const int per_light = 6 * kGMaskTexels * kGMaskTexels;
+        for (int w = 0; w < S.gwords; ++w) {
+            uint64_t cand = 0u;
+            if (need && !hit) {
+                cand = texel >= 0 ? S.gmask[(static_cast<size_t>(slot) * per_light + texel) * S.gwords + w] : ~uint64_t{0};
+                const int rest = S.ns - 64 * w;
+                if (rest < 64) cand &= (uint64_t{1} << rest) - 1u;
+            }
+            while (__any(cand != 0u)) {
+                if (cand) {
+                    exact(64 * w + __builtin_ctzll(cand));
+                    cand = hit ? 0u : cand & (cand - 1u);
+                }
+            }
+            if (!__any(need && !hit)) break;
         }
         return hit;
     }
@@ -786,10 +814,12 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
         // its direction-mask texel, looked up ahead of the shading math so
         // the LDS read overlaps it (p - L = -sdir)
-        const uint64_t smask =
-            S.dmask && valid ? direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
-                                              S.dmask_bytes, muls(sdir, -1.0f), S.ns)
-                             : 0u;
+        uint64_t smask = 0u;  // LDS masks: the mask; wide masks: the texel
+        if (S.dmask && valid)
+            smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
+                                   S.dmask_bytes, muls(sdir, -1.0f), S.ns);
+        else if (S.gmask && valid)
+            smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
         const v3 ldir = normalize(sdir);
         const v3 lref = normalize(reflect(muls(ldir, -1.0f), c.n));
         const float cos_theta = dot(ldir, c.n);
@@ -821,7 +851,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         continue;
 #endif
         if (__any(need)) {
-            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, smask, need);
+            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need);
             if (need && !shadowed) {
                 dif = nd;
                 spe = ns;
@@ -1277,6 +1307,10 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.dmask = p.off_dmask >= 0 ? reinterpret_cast<const char *>(lds + p.off_dmask) : nullptr;
     S.dmask_n = p.dmask_n;
     S.dmask_bytes = p.dmask_bytes;
+    // (recursive depths only: the depth-0/1 kernels keep their register
+    // budget and use the per-wave cone for such scenes)
+    S.gmask = kDepth >= 2 && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
+    S.gwords = p.gmask_words;
     S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
     S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
     S.nbvh = p.n_bvh;

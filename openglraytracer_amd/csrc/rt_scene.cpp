@@ -506,7 +506,7 @@ static void view_frame_setup(const LaunchParams &p, const FrameView &V, const fl
 // than 90 degrees is convex, so holding the corners it holds the square).
 static void build_direction_masks(const std::vector<SphereRec> &sph, const std::vector<SphereMeta> &smeta,
                            const rt_light *lights, const std::vector<LightRec> &lrec, int n,
-                           std::vector<uint64_t> &out) {
+                           std::vector<uint64_t> &out, int words = 1) {
     const int n_lights = static_cast<int>(lrec.size());
     out.clear();
     auto unit = [](double v[3]) {
@@ -555,10 +555,11 @@ static void build_direction_masks(const std::vector<SphereRec> &sph, const std::
                         unit(q);
                         alpha = std::max(alpha, angle(w, q));
                     }
-                    uint64_t bits = 0;
+                    const size_t at = out.size();
+                    out.resize(at + words, 0u);
                     for (size_t s = 0; s < sph.size(); ++s)
-                        if (every[s] || angle(w, &ax[3 * s]) <= alpha + half[s] + 1e-3) bits |= uint64_t{1} << s;
-                    out.push_back(bits);
+                        if (every[s] || angle(w, &ax[3 * s]) <= alpha + half[s] + 1e-3)
+                            out[at + s / 64] |= uint64_t{1} << (s % 64);
                 }
         }
     }
@@ -748,7 +749,19 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         cones.clear();
     }
     ds.n_bvh = static_cast<int32_t>(bvh.size());
-    ds.blob_units = off;
+    ds.blob_units = off;  // the part every work-group stages into LDS
+    // Scenes above kMaskMaxSpheres: wide direction masks (kGMaskMaxSpheres),
+    // kept in the device blob past the staged part and read through L2.
+    std::vector<uint64_t> gmask;
+    ds.off_gmask = -1;
+    ds.gmask_words = 0;
+    if (ds.dmask_n == 0 && sph.size() > static_cast<size_t>(kMaskMaxSpheres) &&
+        sph.size() <= static_cast<size_t>(kGMaskMaxSpheres) && n_live > 0) {
+        ds.gmask_words = static_cast<int32_t>((sph.size() + 63) / 64);
+        build_direction_masks(sph, smeta, lights, lrec, kGMaskTexels, gmask, ds.gmask_words);
+        ds.off_gmask = off;
+        off += units(gmask.size() * 8);
+    }
     ds.n_spheres = static_cast<int32_t>(sph.size());
     ds.n_boxes = static_cast<int32_t>(boxes.size());
     ds.n_mats = n_mats;
@@ -766,6 +779,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     put(ds.off_bvh, bvh.data(), bvh.size() * sizeof(BvhNode));
     if (ds.off_cone >= 0) put(ds.off_cone, cones.data(), cones.size() * sizeof(ShadowCone));
     if (ds.off_dmask >= 0) put(ds.off_dmask, dmask_bytes.data(), dmask_bytes.size());
+    if (ds.off_gmask >= 0) put(ds.off_gmask, gmask.data(), gmask.size() * 8);
     return RT_OK;
 }
 
