@@ -528,10 +528,12 @@ def test_animated_frames_in_one_launch(gpu_ctx):
         s.close()
 
 
-@pytest.mark.parametrize("n_spheres", [3, 16, 17, 32, 33])
+@pytest.mark.parametrize("n_spheres", [3, 16, 17, 32, 33, 64, 65, 130, 256, 257])
 def test_shadow_direction_masks(gpu_ctx, n_spheres):
     """Shadow-ray direction masks (rt_internal.h, kMaskMaxSpheres): 16-bit
-    masks up to 16 spheres, 32-bit up to 32, the per-wave cone above. Spheres
+    masks up to 16 spheres, 32-bit up to 32, 64-bit up to 64 (staged in LDS);
+    wide masks of 2-4 words read through L2 for 65-256 (kGMaskMaxSpheres);
+    the per-wave cone above 256. Spheres
     cluster around the lights (one light inside a sphere, one grazing a
     surface) so that many shadow rays are blocked; culling on and off and the
     oracle must agree bit for bit, at depth 0 and through reflections."""
