@@ -91,9 +91,12 @@ constexpr int kMaskMaxSpheres = 64;
 constexpr size_t kMaskLdsBudget = 19 * 1024;
 // Larger scenes (up to kGMaskMaxSpheres) use the same masks as 64-bit words
 // per texel, kGMaskTexels per face edge, in the device blob after the part
-// the work-groups stage (read through L2: config 4, 256 spheres, 2 x 96 KB).
+// the work-groups stage (read through L2: 256 spheres, 192 KB per live light at 32 texels).
 constexpr int kGMaskMaxSpheres = 256;
-constexpr int kGMaskTexels = 16;
+#ifndef RT_GMASK_TEXELS
+#define RT_GMASK_TEXELS 32  // tuning knob (tools/ablate.sh flags); 8/16/24/32/48/64: config 4 28.2/25.9/25.2/25.0/24.9/24.8 ms
+#endif
+constexpr int kGMaskTexels = RT_GMASK_TEXELS;
 // Sphere BVH node (depth-first order; the left child is the next node):
 // lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
 // this subtree (-1: end) and leaf = (count << 24) | first sphere slot (0 for
