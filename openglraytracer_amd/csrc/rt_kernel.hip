@@ -815,11 +815,11 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         // its direction-mask texel, looked up ahead of the shading math so
         // the LDS read overlaps it (p - L = -sdir)
         uint64_t smask = 0u;  // LDS masks: the mask; wide masks: the texel
-        if (S.dmask && valid)
+        if (S.gmask && valid)  // wide masks win where both exist (as in occluded)
+            smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
+        else if (S.dmask && valid)
             smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
                                    S.dmask_bytes, muls(sdir, -1.0f), S.ns);
-        else if (S.gmask && valid)
-            smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
         const v3 ldir = normalize(sdir);
         const v3 lref = normalize(reflect(muls(ldir, -1.0f), c.n));
         const float cos_theta = dot(ldir, c.n);

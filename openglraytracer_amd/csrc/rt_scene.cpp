@@ -750,12 +750,16 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     }
     ds.n_bvh = static_cast<int32_t>(bvh.size());
     ds.blob_units = off;  // the part every work-group stages into LDS
-    // Scenes above kMaskMaxSpheres: wide direction masks (kGMaskMaxSpheres),
+    // Scenes above RT_GMASK_FROM spheres: wide direction masks (kGMaskMaxSpheres),
+    // also beside the LDS masks (depth 0-1 keep those; depth >= 2 reads these),
     // kept in the device blob past the staged part and read through L2.
     std::vector<uint64_t> gmask;
     ds.off_gmask = -1;
     ds.gmask_words = 0;
-    if (ds.dmask_n == 0 && sph.size() > static_cast<size_t>(kMaskMaxSpheres) &&
+#ifndef RT_GMASK_FROM
+#define RT_GMASK_FROM 32  // wide masks above this many spheres at depth >= 2 (tools/ablate.sh flags; config 3, 64 spheres: 1.15 -> 1.11 ms)
+#endif
+    if (sph.size() > static_cast<size_t>(RT_GMASK_FROM) &&
         sph.size() <= static_cast<size_t>(kGMaskMaxSpheres) && n_live > 0) {
         ds.gmask_words = static_cast<int32_t>((sph.size() + 63) / 64);
         build_direction_masks(sph, smeta, lights, lrec, kGMaskTexels, gmask, ds.gmask_words);

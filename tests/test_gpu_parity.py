@@ -532,7 +532,8 @@ def test_animated_frames_in_one_launch(gpu_ctx):
 def test_shadow_direction_masks(gpu_ctx, n_spheres):
     """Shadow-ray direction masks (rt_internal.h, kMaskMaxSpheres): 16-bit
     masks up to 16 spheres, 32-bit up to 32, 64-bit up to 64 (staged in LDS);
-    wide masks of 2-4 words read through L2 for 65-256 (kGMaskMaxSpheres);
+    wide masks of 1-4 words read through L2 at depth >= 2 for 33-256
+    (RT_GMASK_FROM, kGMaskMaxSpheres; 33-64 keep the LDS masks at depth 0);
     the per-wave cone above 256. Spheres
     cluster around the lights (one light inside a sphere, one grazing a
     surface) so that many shadow rays are blocked; culling on and off and the
