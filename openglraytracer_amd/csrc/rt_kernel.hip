@@ -1309,7 +1309,10 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.dmask_bytes = p.dmask_bytes;
     // (recursive depths only: the depth-0/1 kernels keep their register
     // budget and use the per-wave cone for such scenes)
-    S.gmask = kDepth >= 2 && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
+#ifndef RT_GMASK_MINDEPTH
+#define RT_GMASK_MINDEPTH 2
+#endif
+    S.gmask = kDepth >= RT_GMASK_MINDEPTH && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
     S.gwords = p.gmask_words;
     S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
     S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
