@@ -187,6 +187,7 @@ class Context:
         self._h = C.c_void_p()
         _check(lib().rt_create(device, C.byref(self._h)))
         self.device = device
+        self.output = abi.RT_OUTPUT_RGBA32F  # RT_OPT_OUTPUT (set_output)
 
     def close(self):
         if self._h:
@@ -270,11 +271,24 @@ class Scene:
         return self._h
 
 
+def surface(fmt, *shape):
+    """A zeroed host array for `shape` pixels in surface format `fmt`
+    (RT_OPT_OUTPUT): float32 x4 (RGBA32F), float32 x3 (RGB32F) or uint8 x4
+    (RGBA8)."""
+    if fmt == abi.RT_OUTPUT_RGBA8:
+        return np.zeros(shape + (4,), np.uint8)
+    if fmt == abi.RT_OUTPUT_RGB32F:
+        return np.zeros(shape + (3,), np.float32)
+    return np.zeros(shape + (4,), np.float32)
+
+
 def render(ctx, scene, width, height, max_depth=0, time=0.0, camera=None, view=None, rows=None):
-    """Render rows [r0, r1) to a host array (r1-r0, width, 4) float32,
-    synchronously (the reference's glDispatchCompute + glFinish)."""
+    """Render rows [r0, r1) to a host array, synchronously (the reference's
+    glDispatchCompute + glFinish): (r1-r0, width, C) in the context's surface
+    format (ctx.set_output): float32 RGBA (default), float32 RGB or uint8
+    RGBA."""
     r0, r1 = rows if rows is not None else (0, height)
-    out = np.zeros((max(r1 - r0, 1), max(width, 1), 4), np.float32)  # the C-ABI validates the range
+    out = surface(ctx.output, max(r1 - r0, 1), max(width, 1))  # the C-ABI validates the range
     if view is None:
         view = make_view(camera, time)
     _check(lib().rt_render_view(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
@@ -302,8 +316,9 @@ def render_rgba8(ctx, scene, width, height, max_depth=0, time=0.0, camera=None, 
 
 def render_device(ctx, scene, out_ptr, width, height, max_depth=0, view=None, rows=None,
                   stream=None):
-    """Render into device memory `out_ptr` (e.g. torch tensor.data_ptr()); with
-    `stream` (a hipStream_t as int) the call is asynchronous on that stream."""
+    """Render into device memory `out_ptr` (e.g. torch tensor.data_ptr()),
+    laid out (rows, width, C) in the context's surface format; with `stream`
+    (a hipStream_t as int) the call is asynchronous on that stream."""
     r0, r1 = rows if rows is not None else (0, height)
     if view is None:
         view = make_view(None, 0.0)
@@ -315,7 +330,8 @@ def render_device(ctx, scene, out_ptr, width, height, max_depth=0, view=None, ro
 def render_batch(ctx, scene, out_ptr, width, height, max_depth, views, block_rows=8, n_shards=1,
                  shard=0, stream=None):
     """K frames (K = len(views) <= 8) in one launch into device memory laid
-    out (K, rows, width, 4); rows = height, or this shard's rows."""
+    out (K, rows, width, C) (C and dtype: the context's surface format);
+    rows = height, or this shard's rows."""
     arr = (View * len(views))(*views)
     _check(lib().rt_render_batch(ctx.handle, scene.handle, arr, len(views), width, height, max_depth,
                                  block_rows, n_shards, shard, C.c_void_p(out_ptr),
@@ -325,7 +341,7 @@ def render_batch(ctx, scene, out_ptr, width, height, max_depth, views, block_row
 def render_batch_scenes(ctx, scenes, out_ptr, width, height, max_depth, views, block_rows=8, n_shards=1,
                         shard=0, stream=None):
     """K animated frames in one launch: views[k] of scenes[k] (same layout),
-    into device memory (K, rows, width, 4)."""
+    into device memory (K, rows, width, C) in the context's surface format."""
     arr = (View * len(views))(*views)
     sarr = (C.c_void_p * len(scenes))(*[s.handle for s in scenes])
     _check(lib().rt_render_batch_scenes(ctx.handle, sarr, arr, len(views), width, height, max_depth, block_rows,
@@ -346,7 +362,8 @@ def render_accumulate(ctx, scene, accum_ptr, width, height, max_depth, spp, samp
 
 def render_shard(ctx, scene, out_ptr, width, height, max_depth, block_rows, n_shards, shard,
                  view=None, stream=None):
-    """Render this shard's interleaved row blocks into device memory."""
+    """Render this shard's interleaved row blocks into device memory
+    (rows, width, C) in the context's surface format."""
     if view is None:
         view = make_view(None, 0.0)
     _check(lib().rt_render_shard(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,

@@ -195,9 +195,12 @@ struct DeviceScene {
 // do not all fit.
 void host_frame_setup(LaunchParams &p, const float4 *const *blobs);
 
-// rt_kernel.hip
-hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t stream);
+// rt_kernel.hip. Clears p.sched when the launch does not use the queued
+// distribution (so the caller knows whether the counter slot is in use).
+hipError_t launch_render(LaunchParams &p, int max_depth, hipStream_t stream);
 size_t lds_bytes(const LaunchParams &p);
+// Self-test of the kernel argument block on the context's stream (rt_create).
+int check_kernarg_block(hipStream_t stream);
 
 // rt_api.cpp
 void set_error(const std::string &msg);
@@ -218,6 +221,12 @@ struct rt_context {
     int n_cu = 0;               // compute units of the device
     int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
     unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots
+    // per slot: an event recorded after the slot's last queued launch; a
+    // launch that reuses the slot waits for it on its own stream, so more
+    // than kSchedSlots queued launches in flight never share counters
+    hipEvent_t sched_done[rtamd::kSchedSlots] = {};
+    bool sched_used[rtamd::kSchedSlots] = {};
+    std::vector<struct rt_scene *> scenes;  // live scenes (detached by rt_destroy)
 };
 
 struct rt_scene {
@@ -225,4 +234,5 @@ struct rt_scene {
     rtamd::DeviceScene dev;
     std::vector<float4> host;    // host copy of the blob (per-frame constants on the host)
     int32_t capacity_units = 0;  // allocated blob size (16-B units)
+    rt_context *ctx = nullptr;   // owning context (nullptr once it is destroyed)
 };

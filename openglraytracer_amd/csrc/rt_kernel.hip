@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <string>
 
 #include "rt_internal.h"
 
@@ -1388,14 +1389,17 @@ int groups_per_cu(const void *fn, size_t lds) {
 }
 
 template <int kDepth, bool kAccum>
-hipError_t launch_kernel(LaunchParams p, hipStream_t stream) {
+hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
     const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
     dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY * kRounds - 1) / (kTileY * kRounds), p.n_views);
     const int wave_tiles = ((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
-    if (kQueuedDepth(kDepth) && p.sched && p.n_views == 1 && wave_tiles > resident * (kThreads / 64)) {
-        grid = dim3(resident, 1, 1);  // queued: more wave tiles than resident waves
+    // queued: more wave tiles than resident waves, and every queue has a
+    // wave (a queue without one would leave its tiles unrendered)
+    if (kQueuedDepth(kDepth) && p.sched && p.n_views == 1 && wave_tiles > resident * (kThreads / 64) &&
+        resident * (kThreads / 64) >= kQueues) {
+        grid = dim3(resident, 1, 1);
     } else {
         p.sched = nullptr;
     }
@@ -1404,7 +1408,7 @@ hipError_t launch_kernel(LaunchParams p, hipStream_t stream) {
 }
 
 template <int kDepth>
-hipError_t launch_depth(const LaunchParams &p, hipStream_t stream) {
+hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
     return p.spp > 0 ? launch_kernel<kDepth, true>(p, stream) : launch_kernel<kDepth, false>(p, stream);
 }
 
@@ -1415,7 +1419,7 @@ size_t lds_bytes(const LaunchParams &p) {
     return (static_cast<size_t>(p.blob_units) + 2 * static_cast<size_t>(p.n_spheres) + p.n_boxes) * sizeof(float4);
 }
 
-hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t stream) {
+hipError_t launch_render(LaunchParams &p, int max_depth, hipStream_t stream) {
     switch (max_depth) {
         case 0: return launch_depth<0>(p, stream);
         case 1: return launch_depth<1>(p, stream);
@@ -1429,6 +1433,43 @@ hipError_t launch_render(const LaunchParams &p, int max_depth, hipStream_t strea
         case 9: return launch_depth<9>(p, stream);
         default: return hipErrorInvalidValue;
     }
+}
+
+// Kernel-argument self-test (rt_create): the launch parameter block is larger
+// than HIP's documented 4 KiB argument limit; a runtime that truncated it
+// would silently corrupt renders. One lane copies the block's last words.
+__global__ void kernarg_probe(LaunchParams p, float4 *out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        out[0] = p.frame_consts[kMaxFrameConsts - 1];
+        out[1] = make_float4(__int_as_float(p.n_frame_consts), __int_as_float(p.out_format), 0.0f, 0.0f);
+    }
+}
+
+int check_kernarg_block(hipStream_t stream) {
+    LaunchParams p{};
+    p.frame_consts[kMaxFrameConsts - 1] = make_float4(1.5f, -2.25f, 3.125f, 4096.0f);
+    p.n_frame_consts = 0x5a5a;
+    p.out_format = 0x3c3c;
+    float4 *d = nullptr, h[2] = {};
+    hipError_t e = hipMalloc(&d, sizeof h);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(kernarg_probe, dim3(1), dim3(64), 0, stream, p, d);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        (void)hipFree(d);
+    }
+    if (e != hipSuccess) {
+        set_error(std::string("rt_create: kernel argument probe: ") + hipGetErrorString(e));
+        return RT_ERR_HIP;
+    }
+    if (h[0].x != 1.5f || h[0].y != -2.25f || h[0].z != 3.125f || h[0].w != 4096.0f ||
+        __builtin_bit_cast(uint32_t, h[1].x) != 0x5a5au || __builtin_bit_cast(uint32_t, h[1].y) != 0x3c3cu) {
+        set_error("rt_create: this HIP runtime does not pass a " + std::to_string(sizeof(LaunchParams)) +
+                  "-byte kernel argument block intact");
+        return RT_ERR_UNSUPPORTED;
+    }
+    return RT_OK;
 }
 
 // Allow dynamic LDS above the 64 KiB default for every depth instantiation

@@ -125,3 +125,22 @@ def assemble_frame(recv, height, width, block_rows, n_shards, channels=4, perm=N
     except ImportError:
         pass
     return cat[perm]
+
+
+def gather_frame(shard, height, width, block_rows, n_shards, rank, channels=4, gather_list=None, perm=None,
+                 dst=0):
+    """One frame row-tiled over the ranks of torch.distributed (SURVEY.md
+    §8(e), config 4): `shard` is this rank's flat buffer of
+    flat_shard_elems(1, ...) elements holding its packed rows (rt_render_shard)
+    at the start. One gather (RCCL over xGMI with the nccl backend) brings
+    every shard to rank `dst`, which de-interleaves them (one index_select)
+    and returns the frame (height, width, channels); other ranks return None.
+    `gather_list` (dst only): n_shards buffers like `shard` to receive into."""
+    import torch.distributed as dist
+    if rank == dst:
+        if gather_list is None:
+            gather_list = [shard.new_empty(shard.shape) for _ in range(n_shards)]
+        dist.gather(shard, gather_list, dst=dst)
+        return assemble(gather_list, 1, height, width, block_rows, channels=channels, perm=perm)[0]
+    dist.gather(shard, None, dst=dst)
+    return None

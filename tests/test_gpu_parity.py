@@ -567,3 +567,64 @@ def test_shadow_direction_masks(gpu_ctx, n_spheres):
         assert np.array_equal(on, off, equal_nan=True), (depth, parity_stats(on, off))
         o = oracle_render(objs, 128, 72, depth, lights=lights)
         assert np.array_equal(on, o, equal_nan=True), (depth, parity_stats(on, o))
+
+
+def test_config5_monte_carlo_kernel_full_frame(gpu_ctx):
+    """The kernel bench.py --workload config5 times (render_kernel<0, true>:
+    max_depth 0, jittered samples): the full 1920x1080 config-5 frame at 4 spp,
+    split in two sample ranges like the sample-sharded multi-GPU step,
+    bitwise equal to the oracle's same-order sums on bands of rows; without
+    jitter every sample is the config-2 frame (main.cpp:228-238: one ray per
+    pixel is the jitter-off limit)."""
+    build, w, h, depth = scenes.CONFIGS["config5"]
+    objs = build()
+    view = rt.make_view(None, 0.0)
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 0, seed=0, view=view)
+        rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 2, seed=0, view=view)
+        one = torch.zeros_like(acc)
+        rt.render_accumulate(gpu_ctx, sc, one.data_ptr(), w, h, depth, 4, 0, seed=0, view=view)
+        torch.cuda.synchronize()
+        split, whole = acc.cpu().numpy(), one.cpu().numpy()
+        assert np.isfinite(split).all() and (split[..., 3] == 0).all()
+        for r0, r1 in [(0, 4), (538, 542), (1076, 1080)]:
+            o = port.render_accumulate(objs, w, h, depth, 2, 0, seed=0, rows=(r0, r1))
+            o = port.render_accumulate(objs, w, h, depth, 2, 2, seed=0, rows=(r0, r1), accum=o)
+            assert np.array_equal(split[r0:r1], o), (r0, parity_stats(split[r0:r1], o))
+            o1 = port.render_accumulate(objs, w, h, depth, 4, 0, seed=0, rows=(r0, r1))
+            assert np.array_equal(whole[r0:r1], o1), (r0, parity_stats(whole[r0:r1], o1))
+        # the two orders differ only by float re-association
+        assert np.allclose(split, whole, rtol=1e-6, atol=1e-6)
+        one.zero_()
+        rt.render_accumulate(gpu_ctx, sc, one.data_ptr(), w, h, depth, 2, 0, jitter=False, view=view)
+        f = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+        assert np.array_equal(one.cpu().numpy(), f + f)
+    finally:
+        sc.close()
+
+
+@pytest.mark.parametrize("fmt", [rt.abi.RT_OUTPUT_RGBA32F, rt.abi.RT_OUTPUT_RGB32F, rt.abi.RT_OUTPUT_RGBA8])
+def test_render_returns_the_context_surface_format(gpu_ctx, fmt):
+    """rt.render() sizes its host array from the context's surface format
+    (RT_OPT_OUTPUT): float RGBA, packed float RGB or GL_RGBA8 bytes."""
+    objs = scenes.bench_objects(16)
+    w, h = 200, 120
+    view = rt.make_view(None, 0.0)
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        ref = rt.render(gpu_ctx, sc, w, h, 1, view=view)
+        gpu_ctx.set_output(fmt)
+        got = rt.render(gpu_ctx, sc, w, h, 1, view=view, rows=(10, 90))
+    finally:
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA32F)
+        sc.close()
+    if fmt == rt.abi.RT_OUTPUT_RGBA8:
+        assert got.dtype == np.uint8 and got.shape == (80, w, 4)
+        assert np.array_equal(got, rt.pack_rgba8(ref[10:90]))
+    elif fmt == rt.abi.RT_OUTPUT_RGB32F:
+        assert got.dtype == np.float32 and got.shape == (80, w, 3)
+        assert np.array_equal(got, ref[10:90, :, :3])
+    else:
+        assert np.array_equal(got, ref[10:90])

@@ -2,7 +2,7 @@
 
     python tools/ab.py CONFIG[,CONFIG...] BUILD [BUILD ...]
 
-BUILD is a directory under tools/_ablate (tools/ablate.sh) or "main" for the
+BUILD is a directory under _ab (tools/ablate.sh) or "main" for the
 in-tree library. Every build gets its own context and scene; each round times
 every build once (one event pair around REPS back-to-back launches on a
 non-default stream), rounds interleaved so clock drift hits all builds alike.
@@ -27,7 +27,7 @@ ROUNDS = 7
 
 
 def load(name):
-    path = rt.LIB_PATH if name == "main" else os.path.join(ROOT, "tools", "_ablate", name, "libopenglraytracer_amd.so")
+    path = rt.LIB_PATH if name == "main" else os.path.join(ROOT, "_ab", name, "libopenglraytracer_amd.so")
     L = C.CDLL(path)
     vp, i = C.c_void_p, C.c_int
     L.rt_create.argtypes = [i, vp]

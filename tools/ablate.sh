@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing-only builds of the kernel into tools/_ablate/<name>/:
+# Timing-only builds of the kernel into _ab/<name>/ (delete _ab/ after use: it travels with every gpurun call):
 #   tools/ablate.sh            ablation variants (outputs wrong by design)
 #   tools/ablate.sh rev REV    the library as of git revision REV (A/B timing
 #                              against the working tree in one GPU call)
@@ -7,13 +7,13 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 build() {  # name srcdir extra-flags
-  local out=tools/_ablate/$1; mkdir -p $out/obj
+  local out=_ab/$1; mkdir -p $out/obj
   make -s -C "$2" OBJDIR=$(pwd)/$out/obj OUT=$(pwd)/$out/libopenglraytracer_amd.so CLI=/dev/null \
        FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize $3" $(pwd)/$out/libopenglraytracer_amd.so
 }
 if [ "${1:-}" = rev ]; then
-  rev=${2:?revision}; src=tools/_ablate/rev_src
-  rm -rf $src tools/_ablate/rev; mkdir -p $src/pkg/csrc $src/include
+  rev=${2:?revision}; src=_ab/rev_src
+  rm -rf $src _ab/rev; mkdir -p $src/pkg/csrc $src/include
   for f in $(git ls-tree --name-only $rev openglraytracer_amd/csrc/); do git show $rev:$f > $src/pkg/csrc/$(basename $f); done
   git show $rev:include/rt.h > $src/include/rt.h
   build rev $src/pkg/csrc ""

@@ -18,7 +18,7 @@ from oracle import scenes
 name = sys.argv[1]
 cfgs = sys.argv[2:] or ["config2"]
 if name != "main":  # "main": the in-tree library
-    rt.LIB_PATH = os.path.join(ROOT, "tools", "_ablate", name, "libopenglraytracer_amd.so")
+    rt.LIB_PATH = os.path.join(ROOT, "_ab", name, "libopenglraytracer_amd.so")
 ctx = rt.Context(0)
 view = rt.make_view(None, 0.0)
 stream = torch.cuda.Stream()  # non-default: the C-ABI runs NULL-stream calls synchronously

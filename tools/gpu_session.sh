@@ -1,0 +1,34 @@
+#!/bin/bash
+# One GPU-box session (run through gpurun): tests, bench lines and profiles.
+# usage: tools/gpu_session.sh TAG [tests] [bench] [prof] [list]
+set -uo pipefail
+tag=${1:?tag}; shift
+out=gpurun_out/$tag; mkdir -p $out
+export TMPDIR=/tmp
+want() { for a in "${STEPS[@]}"; do [ "$a" = "$1" ] && return 0; done; return 1; }
+STEPS=("$@")
+step() {  # name timeout cmd... ; stops the session on any failure
+  local name=$1 t=$2; shift 2
+  echo "== $name" ; date
+  timeout -k 10 $t "$@" > $out/$name.log 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -3 $out/$name.log
+  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+}
+if want list; then step counters 60 rocprofv3 -L; fi
+if want tests; then step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread; fi
+if want smoke; then step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; fi
+if want bench; then
+  step bench_config2 300 python bench.py
+  step bench_config3 300 python bench.py --workload config3 --steps 20 --warmup 3 --no-cpu-baseline
+  step bench_config4 300 python bench.py --workload config4 --steps 5 --warmup 1 --no-cpu-baseline
+  step bench_config5 300 python bench.py --workload config5 --steps 3 --warmup 1 --no-cpu-baseline
+fi
+if want prof; then
+  step prof_config4 900 tools/profile.sh $tag/c4 --workload config4 --steps 3 --warmup 1
+  step prof_config3 900 tools/profile.sh $tag/c3 --workload config3 --steps 10 --warmup 2
+fi
+if want prof2; then
+  step prof_config2 900 tools/profile.sh $tag/c2 --steps 50 --warmup 5
+fi
+echo done

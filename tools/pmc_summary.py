@@ -5,8 +5,11 @@ gfx950 corrections of /opt/skills/guides/MI355X_MICROARCH.md (§HBM):
 WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores; FETCH_SIZE
 reports half the bytes of a wide coalesced read, so it is doubled.
 
-usage: python tools/pmc_summary.py gpurun_out/prof/r01 profiles/r01 [FRAMES_PER_LAUNCH]
-(FRAMES_PER_LAUNCH: views per render launch of the profiled bench run, default 8)
+usage: python tools/pmc_summary.py gpurun_out/prof/r01 profiles/r01 [FRAMES_PER_LAUNCH] [WORKLOAD]
+(FRAMES_PER_LAUNCH: views per render launch of the profiled bench run, default 8;
+WORKLOAD: bench.py --workload of the run, default config2). Writes
+profiles/pmc_<WORKLOAD>_latest.json (bench.py reads it) and, for config2,
+profiles/pmc_latest.json.
 """
 import csv
 import json
@@ -17,6 +20,7 @@ from collections import defaultdict
 
 src, dst = sys.argv[1], sys.argv[2]
 frames_per_launch = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+workload = sys.argv[4] if len(sys.argv) > 4 else "config2"
 KERNEL = "render_kernel"
 
 
@@ -39,11 +43,33 @@ stats = {}
 for r in csv.DictReader(open(os.path.join(src, "trace_kernel_stats.csv"))):
     stats[r["Name"]] = r
 k = [v for n, v in stats.items() if KERNEL in n]
+# registers and scratch of the dispatched kernel (kernel-trace columns)
+res = {}
+tpath = os.path.join(src, "trace_kernel_trace.csv")
+if os.path.exists(tpath):
+    for r in csv.DictReader(open(tpath)):
+        if KERNEL in r.get("Kernel_Name", ""):
+            for key in ("VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "Private_Segment_Size", "Scratch_Size",
+                        "LDS_Block_Size", "Group_Segment_Size"):
+                if key in r and r[key] != "":
+                    res[key] = r[key]
+            break
+build = None
+blog = os.path.join(src, "bench_trace.log")
+if os.path.exists(blog):
+    for line in open(blog):
+        if line.startswith("{"):
+            try:
+                build = json.loads(line).get("build")
+            except ValueError:
+                pass
 w, f, sq, cyc = counters("pmc_write"), counters("pmc_fetch"), counters("pmc_sq"), counters("pmc_cyc")
 write_b = mean(w.get("WRITE_SIZE", [])) * 1024 if w.get("WRITE_SIZE") else None
 fetch_b = mean(f.get("FETCH_SIZE", [])) * 1024 * 2 if f.get("FETCH_SIZE") else None
 out = {
-    "workload": "config2", "n_gpus": 1, "frames_per_launch": frames_per_launch,
+    "workload": workload, "n_gpus": 1, "frames_per_launch": frames_per_launch, "build": build,
+    "kernel_resources": res,
+    "scratch_bytes_per_lane": int(res["Private_Segment_Size"]) if res.get("Private_Segment_Size") else None,
     "kernel": k[0]["Name"] if k else None,
     "avg_kernel_ns": float(k[0]["AverageNs"]) if k else None, "calls": int(k[0]["Calls"]) if k else None,
     "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
@@ -65,10 +91,17 @@ if out["sq_insts_valu_per_launch"] and out["avg_kernel_ns"]:
     # wave64 VALU issue: 2 cycles per instruction per SIMD, 1024 SIMDs
     clk = out.get("effective_clock_ghz") or 2.4
     out["valu_issue_utilisation"] = out["sq_insts_valu_per_launch"] * 2 / (1024 * clk * out["avg_kernel_ns"])
+allc = {}
+for name in ("pmc_write", "pmc_fetch", "pmc_sq", "pmc_cyc"):
+    for cname, vals in counters(name).items():
+        allc[cname] = mean(vals)
+out["counters_per_launch"] = allc
 os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
 with open(dst + "_pmc.json", "w") as fo:
     json.dump(out, fo, indent=1)
 shutil.copy(os.path.join(src, "trace_kernel_stats.csv"), dst + "_kernel_stats.csv")
-with open(os.path.join(os.path.dirname(dst) or ".", "pmc_latest.json"), "w") as fo:
-    json.dump(out, fo, indent=1)
+d = os.path.dirname(dst) or "."
+for name in ["pmc_%s_latest.json" % workload] + (["pmc_latest.json"] if workload == "config2" else []):
+    with open(os.path.join(d, name), "w") as fo:
+        json.dump(out, fo, indent=1)
 print(json.dumps(out, indent=1))

@@ -1,20 +1,22 @@
 #!/bin/bash
 # Profile bench.py on the GPU box (run through gpurun):
 #   kernel trace + stats, then separate PMC passes (HBM write bytes, HBM fetch
-#   bytes, VALU instruction/wave counters) — never combined with tracing of
-#   other domains. Outputs under gpurun_out/prof/<tag>/.
+#   bytes, VALU instruction/wave counters, cycles, scratch/LDS traffic) —
+#   never combined with tracing of other domains. Outputs under
+#   gpurun_out/prof/<tag>/.
 # usage: tools/profile.sh <tag> [bench args...]
 set -euo pipefail
 tag=${1:-r01}; shift || true
-out=gpurun_out/prof/$tag
+out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
 args=("$@")
 [ ${#args[@]} -eq 0 ] && args=(--steps 50 --warmup 5)
 run() { timeout -k 10 300 "$@"; }
+pmc() { local name=$1; shift; timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d "$out" -o "$name" -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_$name.log" 2>&1; }
 run rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o trace -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_trace.log" 2>&1
-run rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out" -o pmc_write -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_pmc_write.log" 2>&1
-run rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out" -o pmc_fetch -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_pmc_fetch.log" 2>&1
-run rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d "$out" -o pmc_sq -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_pmc_sq.log" 2>&1
-run rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$out" -o pmc_cyc -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_pmc_cyc.log" 2>&1
+pmc pmc_write WRITE_SIZE
+pmc pmc_fetch FETCH_SIZE
+pmc pmc_sq SQ_INSTS_VALU SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM
+pmc pmc_cyc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE
 find "$out" -type f | sort
