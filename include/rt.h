@@ -225,6 +225,35 @@ int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *
                          int max_depth, int spp, int sample_offset, uint32_t seed, int jitter, int row_begin,
                          int row_end, float *accum_device, void *hip_stream);
 
+/* ---- one frame on several GPUs of this process ----
+ * The reference renders a frame with one glDispatchCompute(W, H, 1) +
+ * glFinish (OpenGLRaytracer/main.cpp:228-238). A multi-GPU group deals the
+ * frame's rows in interleaved blocks of block_rows rows to its GPUs (the
+ * rt_shard_rows / rt_render_shard layout), every GPU renders its blocks on
+ * its context's stream, one gather brings the shards to the first context's
+ * GPU (the root) — RCCL point-to-point over xGMI (ncclCommInitAll over the
+ * contexts' devices; one context per device) or peer copies — and the root
+ * de-interleaves them into the frame. The result is bit-identical to
+ * rt_render of the whole frame on one GPU. */
+typedef struct rt_multi rt_multi;
+#define RT_MULTI_RCCL 0 /* RCCL grouped ncclSend / ncclRecv to the root */
+#define RT_MULTI_COPY 1 /* hipMemcpyPeerAsync; also serves contexts that share a device */
+/* ctxs[0..n_gpus) stay owned by the caller and must outlive the group. */
+int rt_multi_create(int n_gpus, rt_context *const *ctxs, int transport, rt_multi **out);
+void rt_multi_destroy(rt_multi *m);
+/* scenes[i]: the frame's scene on ctxs[i]'s device (the same content on
+ * every device). out: the whole frame in the root context's surface format
+ * (RT_OPT_OUTPUT, the same on every context), device memory of the root's
+ * GPU if out_is_device, else host memory. Synchronous, like glFinish. */
+int rt_render_multi(rt_multi *m, const rt_scene *const *scenes, const rt_camera *cam, float time, int width,
+                    int height, int max_depth, int block_rows, float *out, int out_is_device);
+int rt_render_multi_view(rt_multi *m, const rt_scene *const *scenes, const rt_view *view, int width, int height,
+                         int max_depth, int block_rows, float *out, int out_is_device);
+/* Times of the last rt_render_multi: kernel_ms[i] per GPU (-1 when its
+ * context's RT_OPT_TIMING is off or it had no rows), the gather (from the
+ * moment every shard is complete) and the de-interleave on the root. */
+int rt_multi_last_ms(rt_multi *m, float *kernel_ms, float *gather_ms, float *assemble_ms);
+
 /* Context options. RT_OPT_CULLING (default 1): skip spheres that provably
  * cannot be hit (conservative footprints / light cones with margins far
  * above float error) — output is bit-identical either way. */

@@ -73,6 +73,10 @@ def lib():
             "rt_write_ppm": ([C.c_char_p, vp, i, i], i), "rt_write_pfm": ([C.c_char_p, vp, i, i], i),
             "rt_last_error": ([], C.c_char_p), "rt_version": ([], C.c_char_p),
             "rt_scene_desc_parse": ([C.c_char_p, f, vp, i, vp, vp, i, vp, vp, i, vp, vp, vp], i),
+            "rt_multi_create": ([i, vp, i, vp], i), "rt_multi_destroy": ([vp], None),
+            "rt_render_multi": ([vp, vp, vp, f, i, i, i, i, vp, i], i),
+            "rt_render_multi_view": ([vp, vp, vp, i, i, i, i, vp, i], i),
+            "rt_multi_last_ms": ([vp, vp, vp, vp], i),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -369,3 +373,54 @@ def render_shard(ctx, scene, out_ptr, width, height, max_depth, block_rows, n_sh
     _check(lib().rt_render_shard(ctx.handle, scene.handle, C.byref(view), width, height, max_depth,
                                  block_rows, n_shards, shard, C.c_void_p(out_ptr),
                                  C.c_void_p(stream) if stream else None))
+
+
+class Multi:
+    """One frame on several GPUs of this process (rt_multi_create /
+    rt_render_multi): interleaved row blocks per context, gathered to the
+    first context's GPU (RCCL, or peer copies with transport=RT_MULTI_COPY,
+    which also serves contexts sharing a device) and de-interleaved there."""
+
+    def __init__(self, contexts, transport=abi.RT_MULTI_RCCL):
+        self.contexts = list(contexts)
+        arr = (C.c_void_p * len(self.contexts))(*[c.handle for c in self.contexts])
+        self._h = C.c_void_p()
+        _check(lib().rt_multi_create(len(self.contexts), arr, transport, C.byref(self._h)))
+
+    def render(self, scenes, width, height, max_depth=0, time=0.0, camera=None, view=None, block_rows=8):
+        """The whole frame as a host array in the root context's surface format."""
+        out = surface(self.contexts[0].output, max(height, 1), max(width, 1))
+        self._render(scenes, width, height, max_depth, time, camera, view, block_rows, out.ctypes.data, 0)
+        return out[:height, :width]
+
+    def render_device(self, scenes, out_ptr, width, height, max_depth=0, time=0.0, camera=None, view=None,
+                      block_rows=8):
+        """The whole frame into device memory of the root context's GPU."""
+        self._render(scenes, width, height, max_depth, time, camera, view, block_rows, out_ptr, 1)
+
+    def _render(self, scenes, width, height, max_depth, time, camera, view, block_rows, ptr, is_device):
+        sarr = (C.c_void_p * len(scenes))(*[s.handle for s in scenes])
+        if view is not None:
+            _check(lib().rt_render_multi_view(self._h, sarr, C.byref(view), width, height, max_depth, block_rows,
+                                              C.c_void_p(ptr), is_device))
+        else:
+            _check(lib().rt_render_multi(self._h, sarr, C.byref(camera) if camera is not None else None, time,
+                                         width, height, max_depth, block_rows, C.c_void_p(ptr), is_device))
+
+    def last_ms(self):
+        """(per-GPU kernel ms, gather ms, assembly ms) of the last render."""
+        k = (C.c_float * len(self.contexts))()
+        g, a = C.c_float(), C.c_float()
+        _check(lib().rt_multi_last_ms(self._h, k, C.byref(g), C.byref(a)))
+        return list(k), g.value, a.value
+
+    def close(self):
+        if self._h:
+            lib().rt_multi_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -26,6 +26,8 @@ RT_OUTPUT_RGBA32F = 0
 RT_OUTPUT_RGBA8 = 1
 RT_OUTPUT_RGB32F = 2
 RT_MAX_BATCH = 8
+RT_MULTI_RCCL = 0
+RT_MULTI_COPY = 1
 
 # material indices of the reference table (raytrace_compute.glsl:74-157)
 MATERIAL1, MATERIAL2, RED_GLASS, GREEN_GLASS, BLUE_GLASS, MIRROR, WALL = range(7)

@@ -6,7 +6,10 @@
 //
 //   rt_cli [--width 1280] [--height 720] [--depth 0] [--time 0] [--frames 1]
 //          [--dt 0.016] [--scene shipped|spheres:N[:seed]|FILE.json] [--ppm out_%04d.ppm]
-//          [--pfm out_%04d.pfm] [--device 0]
+//          [--pfm out_%04d.pfm] [--device 0] [--gpus N [--transport rccl|copy] [--block-rows 8]]
+//
+// --gpus N renders every frame on devices device..device+N-1 with
+// rt_render_multi (row blocks per GPU, RCCL gather to the first GPU).
 #include <chrono>
 #include <fstream>
 #include <sstream>
@@ -36,6 +39,7 @@ std::string frame_name(const std::string &pattern, int k) {
 
 int main(int argc, char **argv) {
     int width = 1280, height = 720, depth = 0, frames = 1, device = 0;  // main.cpp:17-19
+    int gpus = 1, block_rows = 8, transport = RT_MULTI_RCCL;
     float time0 = 0.0f, dt = 1.0f / 60.0f;
     std::string scene = "shipped", ppm, pfm;
     for (int i = 1; i < argc; ++i) {
@@ -54,15 +58,24 @@ int main(int argc, char **argv) {
         else if (a == "--ppm") ppm = next();
         else if (a == "--pfm") pfm = next();
         else if (a == "--device") device = std::atoi(next());
+        else if (a == "--gpus") gpus = std::atoi(next());
+        else if (a == "--block-rows") block_rows = std::atoi(next());
+        else if (a == "--transport") transport = std::strcmp(next(), "copy") == 0 ? RT_MULTI_COPY : RT_MULTI_RCCL;
         else {
             std::fprintf(stderr, "usage: rt_cli [--width W] [--height H] [--depth D] [--time T] [--frames K] "
                                  "[--dt S] [--scene shipped|spheres:N[:seed]|FILE.json] [--ppm PAT] [--pfm PAT] "
-                                 "[--device I]\n");
+                                 "[--device I] [--gpus N] [--transport rccl|copy] [--block-rows B]\n");
             return 2;
         }
     }
-    rt_context *ctx = nullptr;
-    if (rt_create(device, &ctx) != RT_OK) return fail("rt_create");
+    if (gpus < 1) { std::fprintf(stderr, "rt_cli: --gpus must be >= 1\n"); return 2; }
+    std::vector<rt_context *> ctxs(gpus, nullptr);
+    for (int g = 0; g < gpus; ++g)
+        if (rt_create(device + g, &ctxs[g]) != RT_OK) return fail("rt_create");
+    rt_context *ctx = ctxs[0];
+    rt_multi *group = nullptr;
+    if (gpus > 1 && rt_multi_create(gpus, ctxs.data(), transport, &group) != RT_OK) return fail("rt_multi_create");
+    std::vector<rt_scene *> scs(gpus, nullptr);
     std::vector<rt_material> mats(RT_REFERENCE_MATERIALS);
     std::vector<rt_light> lights(RT_REFERENCE_LIGHTS);
     rt_reference_materials(mats.data());
@@ -76,7 +89,6 @@ int main(int argc, char **argv) {
         json = ss.str();
     }
     std::vector<float> frame(static_cast<size_t>(width) * height * 4);
-    rt_scene *sc = nullptr;
     for (int k = 0; k < frames; ++k) {
         const float t = time0 + k * dt;
         std::vector<rt_object> objs;
@@ -106,31 +118,51 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "rt_cli: unknown scene %s\n", scene.c_str());
             return 2;
         }
-        if (!sc) {
-            if (rt_scene_create(ctx, objs.data(), static_cast<int>(objs.size()), mats.data(),
-                                static_cast<int>(mats.size()), lights.data(), static_cast<int>(lights.size()),
-                                &sc) != RT_OK)
-                return fail("rt_scene_create");
-        } else if (rt_scene_update(ctx, sc, objs.data(), static_cast<int>(objs.size()), mats.data(),
-                                   static_cast<int>(mats.size()), lights.data(), static_cast<int>(lights.size())) !=
-                   RT_OK) {
-            return fail("rt_scene_update");
+        for (int g = 0; g < gpus; ++g) {  // the frame's scene on every GPU
+            if (!scs[g]) {
+                if (rt_scene_create(ctxs[g], objs.data(), static_cast<int>(objs.size()), mats.data(),
+                                    static_cast<int>(mats.size()), lights.data(), static_cast<int>(lights.size()),
+                                    &scs[g]) != RT_OK)
+                    return fail("rt_scene_create");
+            } else if (rt_scene_update(ctxs[g], scs[g], objs.data(), static_cast<int>(objs.size()), mats.data(),
+                                       static_cast<int>(mats.size()), lights.data(),
+                                       static_cast<int>(lights.size())) != RT_OK) {
+                return fail("rt_scene_update");
+            }
         }
         const auto t0 = std::chrono::steady_clock::now();
-        if (rt_render(ctx, sc, has_cam ? &cam : nullptr, t, width, height, depth, 0, height, frame.data(), 0,
-                      nullptr) != RT_OK)
+        if (group) {
+            if (rt_render_multi(group, scs.data(), has_cam ? &cam : nullptr, t, width, height, depth, block_rows,
+                                frame.data(), 0) != RT_OK)
+                return fail("rt_render_multi");
+        } else if (rt_render(ctx, scs[0], has_cam ? &cam : nullptr, t, width, height, depth, 0, height, frame.data(),
+                             0, nullptr) != RT_OK) {
             return fail("rt_render");
+        }
         const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        float kms = 0.0f;
-        rt_last_kernel_ms(ctx, &kms);
-        std::printf("frame %d t=%.4f  kernel %.3f ms  call %.3f ms (incl. device->host copy)\n", k, t, kms,
-                    wall * 1e3);
+        if (group) {
+            std::vector<float> kms(gpus, 0.0f);
+            float gms = 0.0f, ams = 0.0f;
+            rt_multi_last_ms(group, kms.data(), &gms, &ams);
+            std::printf("frame %d t=%.4f  kernels", k, t);
+            for (float v : kms) std::printf(" %.3f", v);
+            std::printf(" ms  gather %.3f ms  assembly %.3f ms  call %.3f ms (incl. device->host copy)\n", gms, ams,
+                        wall * 1e3);
+        } else {
+            float kms = 0.0f;
+            rt_last_kernel_ms(ctx, &kms);
+            std::printf("frame %d t=%.4f  kernel %.3f ms  call %.3f ms (incl. device->host copy)\n", k, t, kms,
+                        wall * 1e3);
+        }
         if (!ppm.empty() && rt_write_ppm(frame_name(ppm, k).c_str(), frame.data(), width, height) != RT_OK)
             return fail("rt_write_ppm");
         if (!pfm.empty() && rt_write_pfm(frame_name(pfm, k).c_str(), frame.data(), width, height) != RT_OK)
             return fail("rt_write_pfm");
     }
-    rt_scene_destroy(sc);
-    rt_destroy(ctx);
+    rt_multi_destroy(group);
+    for (int g = 0; g < gpus; ++g) {
+        rt_scene_destroy(scs[g]);
+        rt_destroy(ctxs[g]);
+    }
     return 0;
 }

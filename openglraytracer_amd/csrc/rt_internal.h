@@ -204,6 +204,15 @@ int check_kernarg_block(hipStream_t stream);
 
 // rt_api.cpp
 void set_error(const std::string &msg);
+int hip_fail(const char *what, hipError_t e);  // sets the message, returns RT_ERR_HIP
+int check_render_args(const rt_context *ctx, const rt_scene *scene, int width, int height, int max_depth);
+// launch parameters of n_views views of `scene` on `ctx` (output and rows left to the caller)
+LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views,
+                         int width, int height);
+// launch on `stream` with the context's queue slot and kernel-time events
+int launch(rt_context *ctx, LaunchParams &p, int max_depth, hipStream_t stream);
+// bytes per pixel of a surface format (RT_OUTPUT_*)
+inline size_t surface_bytes(int fmt) { return fmt == RT_OUTPUT_RGBA8 ? 4 : (fmt == RT_OUTPUT_RGB32F ? 12 : 16); }
 
 }  // namespace rtamd
 

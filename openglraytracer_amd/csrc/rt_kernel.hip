@@ -197,6 +197,25 @@ struct Ray {
     v3 start, dir;
 };
 
+// Development probe (RT_STATS builds only, tools/stats.py): event counts per
+// launch, accumulated per wave in LDS and flushed once per wave.
+#ifdef RT_STATS
+constexpr int kStats = 16;
+__device__ unsigned long long rt_stats[kStats];
+__shared__ unsigned rt_stats_lds[16][kStats];
+// lanes for which `c` holds (active lanes only)
+#define RT_STAT(k, c)                                                                          \
+    do {                                                                                       \
+        const uint64_t b_ = __ballot(c);                                                       \
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1)))                                \
+            atomicAdd(&rt_stats_lds[threadIdx.x >> 6][k], static_cast<unsigned>(__popcll(b_))); \
+    } while (0)
+#else
+#define RT_STAT(k, c) \
+    do {              \
+    } while (0)
+#endif
+
 // A record read through the constant address space, dword by dword (scalar
 // loads when the address is wave-uniform).
 template <class T>
@@ -459,6 +478,8 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
 template <bool kPrimary>
 __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
     Hit h{10000.0f, -1, 0, false, mk(0.0f, 0.0f, 0.0f)};
+    RT_STAT(kPrimary ? 0 : 1, valid);
+    RT_STAT(kPrimary ? 13 : 2, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
     for (int b = 0; b < S.nb; ++b) {
         const BoxRec B = cload(S.cbox + b);
         v3 rs;
@@ -494,6 +515,7 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
             while (mask) {
                 const int s = base + __builtin_ctzll(mask);
                 mask &= mask - 1;
+                RT_STAT(6, true);
                 test_sphere(S, s, r.start, d2, qa2, qa4, floor, true, h);
             }
         }
@@ -502,11 +524,14 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         const RayInv q = ray_inv(r);
         int node = valid ? 0 : -1;
         while (node >= 0) {
+            RT_STAT(3, true);
+            RT_STAT(4, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
             const float4 lo = S.bvh[2 * node], hi = S.bvh[2 * node + 1];
             const int leaf = __float_as_int(hi.w);
             if (node_hit(q, lo, hi, h.t)) {
                 if (leaf) {
                     const int first = leaf & 0xFFFFFF, count = leaf >> 24;
+                    RT_STAT(5, true);
                     for (int s = first; s < first + count; ++s)
                         test_sphere(S, s, r.start, d2, qa2, qa4, floor, false, h);
                     node = __float_as_int(lo.w);
@@ -557,6 +582,8 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
                                          uint64_t mask, bool need) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
+    RT_STAT(7, need);
+    RT_STAT(10, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
     for (int b = 0; b < S.nb; ++b)
         if (need && !hit) hit = box_occludes(cload(S.cbox + b), start, dir, light_bit);
     if (!__any(need && !hit)) return hit;
@@ -572,6 +599,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         if (s < 0)
 #endif
         if (need && !hit) {
+            RT_STAT(8, true);
             const float4 c = S.sph[s];
             const v3 oc = sub(start, mk(c.x, c.y, c.z));
             const float qb = dot(d2, oc);
@@ -599,6 +627,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
                 if (rest < 64) cand &= (uint64_t{1} << rest) - 1u;
             }
             while (__any(cand != 0u)) {
+                RT_STAT(9, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (cand) {
                     exact(64 * w + __builtin_ctzll(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
@@ -931,6 +960,7 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
     v3 result = black;
     bool first = true;
     while (__any(!done)) {
+        RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
         const bool valid = !done;
         const bool primary = first;
         const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
@@ -997,6 +1027,140 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
     return result;
 }
 
+// Wave-uniform tree walk (default). All 64 lanes of a wave visit the nodes
+// of the full binary ray tree (reflection child first, then refraction
+// child, as the stack machine does, :979-1030) in the same depth-first order;
+// a node is visited when some lane's own tree contains it, and the lanes
+// whose tree does not ride along inactive (`on` = false). The level is
+// therefore wave-uniform, so each level's frame is a fixed set of registers
+// (selected by a scalar level, no scratch), and the rays a wave traces
+// together are the same kind of ray (primary, reflected at level 1, ...) —
+// more coherent than rays of different tree positions. Per level and lane a
+// frame holds the node's colour (phong, then mixed with the reflection), the
+// pending refraction ray and (material | on | sr | st); whether the level is
+// in its refraction child is one uniform bit.
+struct UFrame {
+    v3 col, rs, rd;
+    int mf;  // material | kOn | kSr | kSt
+};
+constexpr int kOn = 1 << 16, kSr = 1 << 17, kSt = 1 << 18;
+
+__device__ __forceinline__ UFrame pick(bool c, const UFrame &a, const UFrame &b) {
+    UFrame r;
+    r.col = sel(c, a.col, b.col);
+    r.rs = sel(c, a.rs, b.rs);
+    r.rd = sel(c, a.rd, b.rd);
+    r.mf = c ? a.mf : b.mf;
+    return r;
+}
+
+// One frame per level as distinct members (no array: nothing for the
+// compiler to index dynamically, so the frames stay in registers).
+template <int N>
+struct UStack {
+    UFrame head;           // level 0 of this sub-stack
+    UStack<N - 1> tail;    // levels 1..N-1
+    // `level` is wave-uniform: every lane takes the same arm
+    __device__ __forceinline__ UFrame get(int level) const {
+        // value selects field by field (a select between the members'
+        // addresses would pin the frames in memory)
+        return pick(level == 0, head, tail.get(level - 1));
+    }
+    __device__ __forceinline__ void set(int level, const UFrame &v) {
+        head = pick(level == 0, v, head);
+        tail.set(level - 1, v);
+    }
+};
+template <>
+struct UStack<1> {
+    UFrame head;
+    __device__ __forceinline__ UFrame get(int) const { return head; }
+    __device__ __forceinline__ void set(int, const UFrame &v) { head = v; }
+};
+
+template <int kDepth>
+__device__ __forceinline__ v3 trace_tree_u(const Scene &S, Ray ray, bool active) {
+    const v3 black = mk(0.0f, 0.0f, 0.0f);
+    UStack<kDepth> F;
+    uint32_t refr_phase = 0u;  // bit P: level P is in its refraction child (uniform)
+    int level = 0;             // uniform
+    bool on = active;
+    v3 value = black;
+    for (;;) {
+        RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
+        const Hit h = level == 0 ? closest<true>(S, ray, on) : closest<false>(S, ray, on);
+        const bool hit = on && h.obj >= 0;
+        Collision c;
+        c.material = 0;
+        v3 col = black;
+        if (__any(hit)) {
+            c = level == 0 ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
+#ifdef RT_ABLATE_PHONG
+            col = add(c.p, c.n);
+#else
+            col = phong(S, ray, c, hit);
+#endif
+        }
+        value = hit ? col : black;  // a missed ray is black (:962-963)
+        if (level < kDepth) {
+            const MatRec &m = S.mat[c.material];
+            const bool sr = hit && m.reflectivity > 0.0f;   // :979-997
+            const bool st = hit && m.transparency > 0.0f;   // :1001-1030
+            const bool any_sr = __any(sr);
+            if (any_sr || __any(st)) {  // push this node, descend into its first child
+                UFrame fr;
+                fr.col = value;
+                fr.rs = sub(c.p, muls(c.n, 0.001f));
+                float ratio = 1.0f / m.refraction_index;
+                if (c.inside) ratio = 1.0f / ratio;
+                fr.rd = refract(ray.dir, c.n, ratio);
+                fr.mf = c.material | (on ? kOn : 0) | (sr ? kSr : 0) | (st ? kSt : 0);
+                F.set(level, fr);
+                if (any_sr) {
+                    ray.start = add(c.p, muls(c.n, 0.001f));
+                    ray.dir = reflect(ray.dir, c.n);
+                    on = sr;
+                    refr_phase &= ~(1u << level);
+                } else {
+                    ray.start = fr.rs;
+                    ray.dir = fr.rd;
+                    on = st;
+                    refr_phase |= 1u << level;
+                }
+                ++level;
+                continue;
+            }
+        }
+        // this node is finished: fold the finished subtrees into their parents
+        bool next_child = false;
+        while (level > 0) {
+            const int P = level - 1;
+            UFrame fr = F.get(P);
+            const MatRec &m = S.mat[fr.mf & 0xFFFF];
+            const bool f_sr = fr.mf & kSr, f_st = fr.mf & kSt;
+            if (!((refr_phase >> P) & 1u)) {  // back from the reflection child
+                if (f_sr) fr.col = mix(fr.col, value, m.reflectivity);
+                if (__any(f_st)) {  // the refraction child comes next
+                    F.set(P, fr);
+                    refr_phase |= 1u << P;
+                    ray.start = fr.rs;
+                    ray.dir = fr.rd;
+                    on = f_st;
+                    next_child = true;
+                    break;
+                }
+                value = fr.col;
+            } else {  // back from the refraction child
+                value = f_st ? mix(fr.col, value, m.transparency) : fr.col;
+            }
+            on = (fr.mf & kOn) != 0;
+            --level;
+        }
+        if (!next_child) break;
+    }
+    return value;
+}
+
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     if (p.n_shards <= 0) return p.row_begin + local;
     const int blk = local / p.block_rows;
@@ -1040,6 +1204,16 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
     return static_cast<float>(h >> 8) * (1.0f / 16777216.0f);
 }
 
+// The per-lane walk (trace_tree) is the default: at 6 waves per SIMD it
+// measured faster than the wave-uniform walk (trace_tree_u), whose frames
+// stay in registers only above 120 VGPRs (config 4, 7680x4320 depth 4:
+// per-lane 25.0 ms; uniform 32.5 / 25.9 / 27.2 / 33.3 ms at 6 / 5 / 4 / 3
+// waves per SIMD; config 3: 1.139 vs 1.114 / 1.153 / 1.289 / 1.282 ms;
+// frames bit-identical; profiles/r02b_tree_walk_ab.log).
+#ifndef RT_TRACE_TREE
+#define RT_TRACE_TREE trace_tree
+#endif
+
 // Occupancy target per depth: the recursive kernels (depth >= 2) keep the
 // tree walk's frames in scratch either way and hide its latency best at 6
 // waves per SIMD (config 4: 58 -> 37 ms; config 3: 1.52 -> 1.37 ms); depth 0/1
@@ -1048,7 +1222,10 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #ifndef RT_WPE0
 #define RT_WPE0 1
 #endif
-#define RT_WAVES_PER_EU(d) ((d) >= 2 ? 6 : ((d) == 0 ? RT_WPE0 : 1))
+#ifndef RT_WPE_DEEP
+#define RT_WPE_DEEP 6
+#endif
+#define RT_WAVES_PER_EU(d) ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1))
 #endif
 #define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(kDepth))))
 // Reductions over aligned groups of 8 lanes (DPP: quad butterflies, then the
@@ -1168,7 +1345,7 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
 // path computes it while the scene is staged), or nullptr.
 template <int kDepth, bool kAccum>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
-                                                 int z, const Pixel &px, const Ray *pre) {
+                                                 int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
     if (!__any(px.active)) return;
     const int x = px.x, y = px.y, local_row = px.local_row;
@@ -1187,7 +1364,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
     const size_t idx = static_cast<size_t>(local_row) * p.width + x;
 
     if constexpr (!kAccum) {
-        const Ray ray = pre ? *pre : camera_ray(p, V, x, y, 0.0f, 0.0f);
+        const Ray ray = have_pre ? pre : camera_ray(p, V, x, y, 0.0f, 0.0f);
 #if defined(RT_ABLATE_RAYGEN)
         const v3 col = mk(float(x), float(y), 0.0f);
 #elif defined(RT_ABLATE_TRACE)
@@ -1195,7 +1372,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 #else
         v3 col;
         if constexpr (kDepth == 0) col = trace0(S, ray, active);
-        else col = trace_tree<kDepth>(S, ray, active);
+        else col = RT_TRACE_TREE<kDepth>(S, ray, active);
 #endif
         if (active) store_pixel(p, z, idx, col);
     } else {
@@ -1207,7 +1384,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
             const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
             v3 col;
             if constexpr (kDepth == 0) col = trace0(S, camera_ray(p, V, x, y, jx, jy), active);
-            else col = trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active);
+            else col = RT_TRACE_TREE<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active);
             acc = add(acc, col);
         }
         if (active) {
@@ -1278,7 +1455,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     const int own_wy = static_cast<int>(blockIdx.y) * kWavesY + wave / kWavesX;
     const Pixel own = wave_pixel(p, own_wx, own_wy);
     RT_PHASE_AFTER(14, own.y);
-    Ray own_ray;
+    Ray own_ray{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 0.0f)};
     if (!queued && !kAccum) own_ray = camera_ray(p, V, own.x, own.y, 0.0f, 0.0f);
     RT_PHASE_AFTER(15, own_ray.dir.x + own_ray.dir.y + own_ray.dir.z);
     RT_PHASE(10);
@@ -1291,6 +1468,9 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
         frame_setup(p, V, sph_cam, sph_px, box_cam);
     }
     RT_PHASE(12);
+#ifdef RT_STATS
+    if (lane < kStats) rt_stats_lds[wave][lane] = 0u;
+#endif
     __syncthreads();
     RT_PHASE(13);
     Scene S;
@@ -1339,13 +1519,13 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     if (!queued) {
         const int stride_y = static_cast<int>(gridDim.y) * kWavesY;
         if constexpr (!kAccum)
-            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, &own_ray);
+            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, own_ray, true);
         else
-            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, nullptr);
+            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, own_ray, false);
         for (int r = 1; r < kRounds; ++r) {
             const int wy = own_wy + r * stride_y;
             if (wy * 8 >= p.n_rows) break;
-            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, wy, z, wave_pixel(p, own_wx, wy), nullptr);
+            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, wy, z, wave_pixel(p, own_wx, wy), own_ray, false);
         }
         return;
     }
@@ -1355,10 +1535,13 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
         const int wx = queued ? t % wtx : own_wx, wy = queued ? t / wtx : own_wy;
         render_wave_tile<kDepth, kAccum>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
-                                         (queued || kAccum) ? nullptr : &own_ray);
+                                         own_ray, !(queued || kAccum));
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
     RT_PHASE(7);
+#ifdef RT_STATS
+    if (lane < kStats) atomicAdd(&rt_stats[lane], static_cast<unsigned long long>(rt_stats_lds[wave][lane]));
+#endif
     if (!queued) return;
     if (lane == 0 && atomicAdd(done, 1) == q_waves - 1) {
         atomicExch(head, 0);  // every wave of the queue has made its last fetch
@@ -1489,6 +1672,19 @@ hipError_t allow_large_lds(size_t bytes) {
 
 }  // namespace rtamd
 
+#ifdef RT_STATS
+extern "C" int rt_debug_stats(unsigned long long *dst, int clear) {
+    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(rtamd::rt_stats), sizeof(rtamd::rt_stats), 0, hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return -1;
+    if (clear) {
+        void *ptr = nullptr;
+        if (hipGetSymbolAddress(&ptr, HIP_SYMBOL(rtamd::rt_stats)) != hipSuccess) return -1;
+        return hipMemset(ptr, 0, sizeof(rtamd::rt_stats)) == hipSuccess ? 0 : -1;
+    }
+    return 0;
+}
+#endif
 #ifdef RT_PHASE_TRACE
 extern "C" int rt_debug_phase_read(void *dst, size_t bytes) {
     const size_t n = bytes < sizeof(rtamd::rt_phase_buf) ? bytes : sizeof(rtamd::rt_phase_buf);

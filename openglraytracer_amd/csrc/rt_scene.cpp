@@ -310,12 +310,53 @@ int build_node(std::vector<BuildItem> &items, int begin, int end, std::vector<Bv
         n.leaf = ((end - begin) << 24) | begin;
         return id;
     }
-    int axis = 0;
-    for (int a = 1; a < 3; ++a)
-        if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
-    const int mid = (begin + end) / 2;
-    std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
-                     [axis](const BuildItem &x, const BuildItem &y) { return x.c[axis] < y.c[axis]; });
+    // surface-area heuristic: over every axis and every split of the
+    // centroid-sorted items, minimise A(left) N(left) + A(right) N(right)
+    // (a sphere test costs about one node test; ties keep the median split)
+    const int cnt = end - begin;
+    auto area = [](const double *l, const double *h) {
+        const double dx = h[0] - l[0], dy = h[1] - l[1], dz = h[2] - l[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    int best_axis = -1, best_mid = (begin + end) / 2;
+#ifndef RT_BVH_MEDIAN
+    double best = 1e300;
+    std::vector<double> left_area(cnt);
+    for (int a = 0; a < 3; ++a) {
+        std::sort(items.begin() + begin, items.begin() + end,
+                  [a](const BuildItem &x, const BuildItem &y) { return x.c[a] < y.c[a]; });
+        double l[3] = {1e300, 1e300, 1e300}, h[3] = {-1e300, -1e300, -1e300};
+        for (int i = 0; i < cnt; ++i) {
+            for (int k = 0; k < 3; ++k) {
+                l[k] = std::min(l[k], items[begin + i].lo[k]);
+                h[k] = std::max(h[k], items[begin + i].hi[k]);
+            }
+            left_area[i] = area(l, h);  // items [begin, begin + i]
+        }
+        double rl[3] = {1e300, 1e300, 1e300}, rh[3] = {-1e300, -1e300, -1e300};
+        for (int i = cnt - 1; i >= 1; --i) {  // right = [begin + i, end)
+            for (int k = 0; k < 3; ++k) {
+                rl[k] = std::min(rl[k], items[begin + i].lo[k]);
+                rh[k] = std::max(rh[k], items[begin + i].hi[k]);
+            }
+            const double cost = left_area[i - 1] * i + area(rl, rh) * (cnt - i);
+            if (cost < best) {
+                best = cost;
+                best_axis = a;
+                best_mid = begin + i;
+            }
+        }
+    }
+#endif
+    int axis = best_axis;
+    if (axis < 0) {  // median split on the widest centroid axis
+        axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+    }
+    const int mid = best_mid;
+    std::sort(items.begin() + begin, items.begin() + end,
+              [axis](const BuildItem &x, const BuildItem &y) { return x.c[axis] < y.c[axis]; });
     nodes[id].leaf = 0;
     build_node(items, begin, mid, nodes);
     build_node(items, mid, end, nodes);

@@ -126,3 +126,36 @@ def test_monte_carlo_sample_sharding(tmp_path, world):
     ref = oracle_port.render_accumulate(scenes.bench_objects(16), 24, 14, 0, 8, 0, seed=3) / 8
     got = np.load(out)
     assert np.allclose(got, ref, rtol=1e-6, atol=1e-6)
+
+
+def gather_frame_worker(rank, world, port, result_path):
+    """bench.py --workload config4 at N ranks: one frame, interleaved 8-row
+    blocks per rank (packed float3 shards, RT_OUTPUT_RGB32F), one gather to
+    rank 0 (frame.gather_frame), de-interleaved there."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from openglraytracer_amd import frame
+    from oracle import port as oracle_port, scenes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    objs = scenes.bench_objects(64)
+    ids = frame.shard_row_ids(H, BLOCK, world, rank)
+    shard = torch.zeros(frame.flat_shard_elems(1, H, W, BLOCK, world, channels=3), dtype=torch.float32)
+    data = np.concatenate([oracle_port.render(objs, W, H, 2, 0.0, rows=(int(r), int(r) + 1)) for r in ids])[..., :3]
+    shard[: data.size] = torch.from_numpy(np.ascontiguousarray(data).reshape(-1))
+    out = frame.gather_frame(shard, H, W, BLOCK, world, rank, channels=3)
+    if rank == 0:
+        np.save(result_path, out.numpy())
+    else:
+        assert out is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_tiled_frame_gathers_to_rank0(tmp_path, world):
+    from oracle import port as oracle_port, scenes
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(gather_frame_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
+    full = oracle_port.render(scenes.bench_objects(64), W, H, 2, 0.0)[..., :3]
+    assert np.array_equal(np.load(out), full)

@@ -628,3 +628,74 @@ def test_render_returns_the_context_surface_format(gpu_ctx, fmt):
         assert np.array_equal(got, ref[10:90, :, :3])
     else:
         assert np.array_equal(got, ref[10:90])
+
+
+@pytest.mark.parametrize("fmt,block", [(rt.abi.RT_OUTPUT_RGBA32F, 8), (rt.abi.RT_OUTPUT_RGB32F, 3),
+                                       (rt.abi.RT_OUTPUT_RGBA8, 8)])
+def test_multi_gpu_group_equals_single_frame(fmt, block):
+    """rt_render_multi (include/rt.h): the frame's interleaved row blocks on
+    three contexts (peer-copy transport: the three share this box's one GPU),
+    gathered to the root and de-interleaved — bit-identical to rt_render of
+    the whole frame, host and device destinations, every surface format."""
+    build, _, _, depth = scenes.CONFIGS["config4"]
+    objs = build()
+    w, h = 768, 437  # odd height: the last block is partial
+    view = rt.make_view(None, 0.0)
+    ctxs = [rt.Context(0) for _ in range(3)]
+    scs = [rt.Scene(c, objs) for c in ctxs]
+    try:
+        for c in ctxs:
+            c.set_output(fmt)
+        whole = rt.render(ctxs[0], scs[0], w, h, depth, view=view)
+        group = rt.Multi(ctxs, transport=rt.abi.RT_MULTI_COPY)
+        try:
+            got = group.render(scs, w, h, depth, view=view, block_rows=block)
+            assert np.array_equal(got, whole)
+            dt = torch.uint8 if fmt == rt.abi.RT_OUTPUT_RGBA8 else torch.float32
+            dev = torch.zeros(whole.shape, dtype=dt, device="cuda")
+            group.render_device(scs, dev.data_ptr(), w, h, depth, view=view, block_rows=block)
+            assert np.array_equal(dev.cpu().numpy(), whole)
+            k, g, a = group.last_ms()
+            assert len(k) == 3 and all(v > 0 for v in k) and g >= 0 and a > 0
+            # the reference orbit camera at `time` (rt_render_multi, cam = NULL)
+            assert np.array_equal(group.render(scs, w, h, depth, time=0.0, block_rows=block), whole)
+        finally:
+            group.close()
+    finally:
+        for s in scs:
+            s.close()
+        for c in ctxs:
+            c.close()
+
+
+def test_multi_gpu_group_rccl():
+    """The RCCL transport (ncclCommInitAll over the contexts' devices, grouped
+    ncclSend / ncclRecv to the root): on every GPU of the box, one context
+    each; bit-identical to the single-GPU frame. Two contexts on one device
+    are refused (RCCL needs distinct devices)."""
+    n = torch.cuda.device_count()
+    objs = scenes.bench_objects(64)
+    w, h, depth = 640, 360, 2
+    view = rt.make_view(None, 0.0)
+    ctxs = [rt.Context(d) for d in range(n)]
+    scs = [rt.Scene(c, objs) for c in ctxs]
+    try:
+        whole = rt.render(ctxs[0], scs[0], w, h, depth, view=view)
+        group = rt.Multi(ctxs, transport=rt.abi.RT_MULTI_RCCL)
+        try:
+            for block in (8, 16):
+                assert np.array_equal(group.render(scs, w, h, depth, view=view, block_rows=block), whole)
+        finally:
+            group.close()
+        extra = rt.Context(0)
+        try:
+            with pytest.raises(rt.RTError) as e:
+                rt.Multi([ctxs[0], extra], transport=rt.abi.RT_MULTI_RCCL)
+            assert e.value.code == rt.abi.RT_ERR_INVALID
+        finally:
+            extra.close()
+    finally:
+        for s in scs:
+            s.close()
+        for c in ctxs:
+            c.close()
