@@ -195,6 +195,12 @@ struct DeviceScene {
 // do not all fit.
 void host_frame_setup(LaunchParams &p, const float4 *const *blobs);
 
+// rt_camera.cpp: the reference orbit camera as llvmpipe evaluates it
+float gl_sin(float a);  // gallivm's polynomial sin / cos (run-time GLSL sin / cos)
+float gl_cos(float a);
+void reference_orbit(float time, float *speed, float pos[3], float *yaw);
+void reference_view_gl(float time, float unproj[16], float view[16]);
+
 // rt_kernel.hip. Clears p.sched when the launch does not use the queued
 // distribution (so the caller knows whether the counter slot is in use).
 hipError_t launch_render(LaunchParams &p, int max_depth, hipStream_t stream);

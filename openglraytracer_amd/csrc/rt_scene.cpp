@@ -2,12 +2,10 @@
 // restated as C++ data, the frame constants (camera unprojection, per-object
 // transforms) and the device-resident scene blob.
 //
-// Frame constants are evaluated in float64 and rounded once to float32. The
-// reference evaluates them in float32 per ray (raytrace_compute.glsl:366-383,
-// :650-652, :718); the unprojection inverse(proj*view) is ill-conditioned
-// (near/far = 1e-4) and llvmpipe's float result depends on how its compiler
-// re-associates inexact float ops, so no float order reproduces it — float64
-// is the closest independent estimate ("Parity").
+// The reference orbit camera's unprojection is evaluated as the reference's
+// GL evaluates it (rt_camera.cpp, bit-identical to llvmpipe). The per-object
+// transforms (:650-652, :718) and explicit cameras are evaluated in float64
+// and rounded once to float32 ("Parity").
 // Everything the kernel evaluates per pixel stays float32 in GLSL order.
 #include <algorithm>
 #include <cmath>
@@ -199,27 +197,24 @@ int rt_reference_objects(float time, rt_object out[RT_REFERENCE_OBJECTS]) {
     float zero[3] = {0, 0, 0};
     float mn0[3] = {-11, -11, -11}, mx0[3] = {11, 11, 11};
     make_object(out[0], mn0, mx0, -1.0f, 0, 0, 0, 0, 0, 0, RT_MAT_WALL);
-    const float s = 0.5f * std::sin(st * 0.5f) + 1.5f;
+    // run-time sin as the reference's GL evaluates it (rt_camera.cpp)
+    const float s = 0.5f * gl_sin(st * 0.5f) + 1.5f;
     float mn1[3] = {-1.0f * s, -1.0f * s, -1.0f * s}, mx1[3] = {1.0f * s, 1.0f * s, 1.0f * s};
-    make_object(out[1], mn1, mx1, -1.0f, 0, 0, std::sin(st * 3.0f), 0, st * 90.0f, 0, RT_MAT_MIRROR);
+    make_object(out[1], mn1, mx1, -1.0f, 0, 0, gl_sin(st * 3.0f), 0, st * 90.0f, 0, RT_MAT_MIRROR);
     float mn2[3] = {-10, -10, -1}, mx2[3] = {10, 10, 1};
-    make_object(out[2], mn2, mx2, -1.0f, 0, 0, -3, std::sin(st * 5.0f) * 10.0f, 45.0f, 0, RT_MAT_GREEN_GLASS);
+    make_object(out[2], mn2, mx2, -1.0f, 0, 0, -3, gl_sin(st * 5.0f) * 10.0f, 45.0f, 0, RT_MAT_GREEN_GLASS);
     float mn3[3] = {-1, -1, -2}, mx3[3] = {1, 1, 2};
     make_object(out[3], mn3, mx3, -1.0f, 3, 4, 1, 45.0f + st * 45.0f, 0, 45.0f + st * 180.0f, RT_MAT_BLUE_GLASS);
     make_object(out[4], zero, zero, 2.0f, -3, 4, 1, 0, 0, 0, RT_MAT_RED_GLASS);
     return RT_OK;
 }
 
-// raytrace_compute.glsl:334-364
+// raytrace_compute.glsl:334-364 (run-time sin / cos and mod() as the
+// reference's GL evaluates them, rt_camera.cpp)
 int rt_reference_camera(float time, rt_camera *out) {
     if (!out) { set_error("rt_reference_camera: null out"); return RT_ERR_INVALID; }
-    const float radius = 10.0f;
-    const float speed = time * 0.4f + 0.5f;
-    out->position[0] = radius * std::cos(speed);
-    out->position[1] = radius * std::sin(speed);
-    out->position[2] = 0.0f;
-    const float x = 1.0f * speed * (180.0f / 3.1416f);
-    const float yaw = (x - 360.0f * std::floor(x / 360.0f)) + 90.0f;  // GLSL mod
+    float yaw;
+    reference_orbit(time, nullptr, out->position, &yaw);
     out->angles[0] = 0.0f;
     out->angles[1] = yaw;
     out->angles[2] = 0.0f;
@@ -251,12 +246,20 @@ int rt_bench_objects(int n_spheres, uint64_t seed, rt_object *out) {
 }
 
 // main() :366-392 — P (:411-426) and V = inverse(T * R * Rx(90)) (:538-545),
-// unprojection = inverse(P * V), all in float64, rounded once.
+// unprojection = inverse(P * V).
+//  cam == NULL: the reference orbit camera at `time`, evaluated as the
+//    reference's GL evaluates it (rt_camera.cpp) — bit-identical to llvmpipe;
+//  an explicit camera (no counterpart in the reference, which hard-codes its
+//    camera): float64, rounded once.
 int rt_make_view(const rt_camera *cam_in, float time, rt_view *out) {
     if (!out) { set_error("rt_make_view: null out"); return RT_ERR_INVALID; }
-    rt_camera cam;
-    if (cam_in) cam = *cam_in;
-    else rt_reference_camera(time, &cam);
+    if (!cam_in) {
+        float speed, yaw;
+        reference_orbit(time, &speed, out->origin, &yaw);  // ray start = c.position (:391)
+        reference_view_gl(time, out->unprojection, nullptr);
+        return RT_OK;
+    }
+    const rt_camera cam = *cam_in;
     const double q = 1.0 / std::tan(static_cast<double>(kDegToRad * 0.5f * cam.v_fov));
     const double n = cam.near_plane, f = cam.far_plane;
     M4 P{};

@@ -358,6 +358,22 @@ static m4 camera_unprojection(const rt_camera *c) {
     dm4 V = d_inverse(d_mul(d_transform(ld3(c->position), ld3(c->angles)), d_rot(0, 90.0f)));
     return d_round(d_inverse(d_mul(P, V)));
 }
+/* the frame's unprojection: pinned, or the reference orbit camera as
+ * llvmpipe computes it (cam == NULL), or an explicit camera in float64 */
+static void gl_reference_matrices(float time, m4 *inv, m4 *view, m4 *proj);
+static m4 frame_unprojection(const rt_camera *cam, float time) {
+    if (g_pinned_unproj || cam) {
+        rt_camera c;
+        if (!cam) {
+            oracle_reference_camera(time, &c);
+            cam = &c;
+        }
+        return camera_unprojection(cam);
+    }
+    m4 inv;
+    gl_reference_matrices(time, &inv, NULL, NULL);
+    return inv;
+}
 static void object_transforms(v3 pos, v3 ang, m4 *l2w, m4 *w2l, m3 *nrm) {
     if (!g_f64_frame) {
         *l2w = calc_transform_matrix(pos, ang);
@@ -414,15 +430,188 @@ static void set_obj(rt_object *o, v3 mins, v3 maxs, float radius, v3 pos, v3 ang
     o->material = mat;
 }
 
+/* ---- the reference orbit camera as llvmpipe compiles it ----------------
+ * (DESIGN.md "Parity"; pinned by tests/golden/camera_llvmpipe.npz, made by
+ * tests/golden/make_camera_golden.py from the reference's own camera
+ * functions.) Run-time sin/cos are gallivm's polynomials with fused
+ * multiply-adds; constant-only terms are folded in float; x*0, x*1, x+0
+ * vanish; (x * #a) * #b becomes x * #(a b); mod()+90 becomes (x + 90) -
+ * 360 floor(x/360); nothing else is fused or reordered. */
+static float gv_sincos(float a, int want_cos) {
+    float xa = fabsf(a);
+    int j = (int)(xa * 1.27323954473516f);
+    int jp = j + 1, je = jp & ~1;
+    float yj = (float)je;
+    uint32_t sign;
+    int poly;
+    if (want_cos) {
+        sign = (uint32_t)((~(je - 2)) & 4) << 29;
+        poly = ((je - 2) & 2) == 0;
+    } else {
+        uint32_t ab;
+        memcpy(&ab, &a, 4);
+        sign = ((uint32_t)(jp & 4) << 29) ^ (ab & 0x80000000u);
+        poly = (je & 2) == 0;
+    }
+    float x = fmaf(yj, -0.78515625f, xa);
+    x = fmaf(yj, -2.4187564849853515625e-4f, x);
+    x = fmaf(yj, -3.77489497744594108e-8f, x);
+    float z = x * x;
+    float c = fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    c = fmaf(c, z, 4.166664568298827e-2f);
+    c = c * z;
+    c = c * z;
+    c = fmaf(z, -0.5f, c);
+    c = c + 1.0f;
+    float sn = fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
+    sn = fmaf(sn, z, -1.6666654611e-1f);
+    sn = sn * z;
+    sn = fmaf(sn, x, x);
+    float r = poly ? sn : c;
+    uint32_t rb;
+    memcpy(&rb, &r, 4);
+    rb ^= sign;
+    memcpy(&r, &rb, 4);
+    return r;
+}
+float oracle_gl_sin(float a) { return gv_sincos(a, 0); }
+float oracle_gl_cos(float a) { return gv_sincos(a, 1); }
+
+/* a value of the compiled camera chain: kind 0 run-time, 1 compile-time
+ * constant, 2 run-time `b` times the constant `k` */
+typedef struct { float v; int kind; float b, k; } gv;
+static gv gv_c(float v) { gv r = {v, 1, 0, 0}; return r; }
+static gv gv_r(float v) { gv r = {v, 0, 0, 0}; return r; }
+static gv gv_neg(gv a) { a.v = -a.v; a.k = -a.k; return a; }
+static gv gv_mul(gv a, gv b) {
+    if (a.kind == 1 && b.kind == 1) return gv_c(a.v * b.v);
+    if (a.kind != 1 && b.kind != 1) return gv_r(a.v * b.v);
+    gv c = a.kind == 1 ? a : b, x = a.kind == 1 ? b : a;
+    if (c.v == 0.0f) return gv_c(0.0f);
+    if (c.v == 1.0f) return x;
+    if (c.v == -1.0f) return gv_neg(x);
+    gv r;
+    r.kind = 2;
+    r.b = x.kind == 2 ? x.b : x.v;
+    r.k = x.kind == 2 ? x.k * c.v : c.v;
+    r.v = r.b * r.k;
+    return r;
+}
+static gv gv_add(gv a, gv b) {
+    if (a.kind == 1 && b.kind == 1) return gv_c(a.v + b.v);
+    if (a.kind == 1 && a.v == 0.0f) return b;
+    if (b.kind == 1 && b.v == 0.0f) return a;
+    return gv_r(a.v + b.v);
+}
+static gv gv_sub(gv a, gv b) { return gv_add(a, gv_neg(b)); }
+typedef struct { gv m[4][4]; } gm; /* m[col][row] */
+static gm gm_ident(void) {
+    gm r;
+    for (int c = 0; c < 4; c++)
+        for (int w = 0; w < 4; w++) r.m[c][w] = gv_c(c == w ? 1.0f : 0.0f);
+    return r;
+}
+static gm gm_mul(gm a, gm b) { /* column c = a0 b.x + a1 b.y + a2 b.z + a3 b.w */
+    gm r;
+    for (int c = 0; c < 4; c++)
+        for (int w = 0; w < 4; w++) {
+            gv acc = gv_mul(a.m[0][w], b.m[c][0]);
+            for (int k = 1; k < 4; k++) acc = gv_add(acc, gv_mul(a.m[k][w], b.m[c][k]));
+            r.m[c][w] = acc;
+        }
+    return r;
+}
+static gv gv_d(gv a, gv b, gv c, gv e) { return gv_sub(gv_mul(a, b), gv_mul(c, e)); }
+static gv gv_t3(gv a, gv x, gv b, gv y, gv c, gv z) { return gv_add(gv_sub(gv_mul(a, x), gv_mul(b, y)), gv_mul(c, z)); }
+static gm gm_inverse(gm A) { /* Mesa's inverse(mat4), as inverse4 above */
+    gv(*m)[4] = A.m;
+    gv S00 = gv_d(m[2][2], m[3][3], m[3][2], m[2][3]), S01 = gv_d(m[2][1], m[3][3], m[3][1], m[2][3]);
+    gv S02 = gv_d(m[2][1], m[3][2], m[3][1], m[2][2]), S03 = gv_d(m[2][0], m[3][3], m[3][0], m[2][3]);
+    gv S04 = gv_d(m[2][0], m[3][2], m[3][0], m[2][2]), S05 = gv_d(m[2][0], m[3][1], m[3][0], m[2][1]);
+    gv S06 = gv_d(m[1][2], m[3][3], m[3][2], m[1][3]), S07 = gv_d(m[1][1], m[3][3], m[3][1], m[1][3]);
+    gv S08 = gv_d(m[1][1], m[3][2], m[3][1], m[1][2]), S09 = gv_d(m[1][0], m[3][3], m[3][0], m[1][3]);
+    gv S10 = gv_d(m[1][0], m[3][2], m[3][0], m[1][2]), S11 = gv_d(m[1][1], m[3][3], m[3][1], m[1][3]);
+    gv S12 = gv_d(m[1][0], m[3][1], m[3][0], m[1][1]), S13 = gv_d(m[1][2], m[2][3], m[2][2], m[1][3]);
+    gv S14 = gv_d(m[1][1], m[2][3], m[2][1], m[1][3]), S15 = gv_d(m[1][1], m[2][2], m[2][1], m[1][2]);
+    gv S16 = gv_d(m[1][0], m[2][3], m[2][0], m[1][3]), S17 = gv_d(m[1][0], m[2][2], m[2][0], m[1][2]);
+    gv S18 = gv_d(m[1][0], m[2][1], m[2][0], m[1][1]);
+    gm a;
+    a.m[0][0] = gv_t3(m[1][1], S00, m[1][2], S01, m[1][3], S02);
+    a.m[1][0] = gv_neg(gv_t3(m[1][0], S00, m[1][2], S03, m[1][3], S04));
+    a.m[2][0] = gv_t3(m[1][0], S01, m[1][1], S03, m[1][3], S05);
+    a.m[3][0] = gv_neg(gv_t3(m[1][0], S02, m[1][1], S04, m[1][2], S05));
+    a.m[0][1] = gv_neg(gv_t3(m[0][1], S00, m[0][2], S01, m[0][3], S02));
+    a.m[1][1] = gv_t3(m[0][0], S00, m[0][2], S03, m[0][3], S04);
+    a.m[2][1] = gv_neg(gv_t3(m[0][0], S01, m[0][1], S03, m[0][3], S05));
+    a.m[3][1] = gv_t3(m[0][0], S02, m[0][1], S04, m[0][2], S05);
+    a.m[0][2] = gv_t3(m[0][1], S06, m[0][2], S07, m[0][3], S08);
+    a.m[1][2] = gv_neg(gv_t3(m[0][0], S06, m[0][2], S09, m[0][3], S10));
+    a.m[2][2] = gv_t3(m[0][0], S11, m[0][1], S09, m[0][3], S12);
+    a.m[3][2] = gv_neg(gv_t3(m[0][0], S08, m[0][1], S10, m[0][2], S12));
+    a.m[0][3] = gv_neg(gv_t3(m[0][1], S13, m[0][2], S14, m[0][3], S15));
+    a.m[1][3] = gv_t3(m[0][0], S13, m[0][2], S16, m[0][3], S17);
+    a.m[2][3] = gv_neg(gv_t3(m[0][0], S14, m[0][1], S16, m[0][3], S18));
+    a.m[3][3] = gv_t3(m[0][0], S15, m[0][1], S17, m[0][2], S18);
+    gv det = gv_add(gv_mul(m[0][0], a.m[0][0]),
+                    gv_add(gv_mul(m[0][1], a.m[1][0]), gv_add(gv_mul(m[0][2], a.m[2][0]), gv_mul(m[0][3], a.m[3][0]))));
+    gm r;
+    for (int c = 0; c < 4; c++)
+        for (int w = 0; w < 4; w++) {
+            gv x = a.m[c][w];
+            r.m[c][w] = (x.kind == 1 && det.kind == 1) ? gv_c(x.v / det.v)
+                        : (x.kind == 1 && x.v == 0.0f) ? gv_c(0.0f) : gv_r(x.v / det.v);
+        }
+    return r;
+}
+static gm gm_rot(int axis, gv c, gv s) { /* :444-486 */
+    gm r = gm_ident();
+    if (axis == 0) { r.m[1][1] = c; r.m[1][2] = s; r.m[2][1] = gv_neg(s); r.m[2][2] = c; }
+    if (axis == 1) { r.m[0][0] = c; r.m[0][2] = gv_neg(s); r.m[2][0] = s; r.m[2][2] = c; }
+    if (axis == 2) { r.m[0][0] = c; r.m[0][1] = s; r.m[1][0] = gv_neg(s); r.m[1][1] = c; }
+    return r;
+}
+/* inverse(proj_mat * view_mat) (:383), view_mat (:368) and proj_mat of the
+ * orbit camera at `time` as llvmpipe computes them */
+static void gl_reference_matrices(float time, m4 *inv, m4 *view, m4 *proj) {
+    float speed = time * 0.4f + 0.5f;                                    /* :343 */
+    float x = speed * (180.0f / 3.1416f);
+    float yaw = (x + 90.0f) - 360.0f * floorf(x / 360.0f);              /* :353 as compiled */
+    float a = DEG_TO_RAD * yaw;
+    gm Rz = gm_rot(2, gv_r(gv_sincos(a, 1)), gv_r(gv_sincos(a, 0)));
+    gm R = gm_mul(gm_mul(gm_mul(gm_ident(), Rz), gm_rot(0, gv_c(1.0f), gv_c(0.0f))), gm_rot(1, gv_c(1.0f), gv_c(0.0f)));
+    gm T = gm_ident();
+    T.m[3][0] = gv_mul(gv_c(10.0f), gv_r(gv_sincos(speed, 1)));
+    T.m[3][1] = gv_mul(gv_c(10.0f), gv_r(gv_sincos(speed, 0)));
+    T.m[3][2] = gv_c(0.0f);
+    float c90 = cosf(DEG_TO_RAD * 90.0f); /* folded at compile time (host libm) */
+    gm V = gm_inverse(gm_mul(gm_mul(T, R), gm_rot(0, gv_c(c90), gv_c(1.0f))));
+    gm P;
+    for (int c = 0; c < 4; c++)
+        for (int w = 0; w < 4; w++) P.m[c][w] = gv_c(0.0f);
+    float q = 1.0f / (sinf(DEG_TO_RAD * 0.5f * 90.0f) / cosf(DEG_TO_RAD * 0.5f * 90.0f)); /* tan = sin/cos, folded */
+    P.m[0][0] = gv_c(q / (16.0f / 9.0f));
+    P.m[1][1] = gv_c(q);
+    P.m[2][2] = gv_c((0.1f + 1000.0f) / (0.1f - 1000.0f));
+    P.m[2][3] = gv_c(-1.0f);
+    P.m[3][2] = gv_c((2.0f * 0.1f * 1000.0f) / (0.1f - 1000.0f));
+    gm U = gm_inverse(gm_mul(P, V));
+    for (int c = 0; c < 4; c++)
+        for (int w = 0; w < 4; w++) {
+            if (inv) inv->m[c][w] = U.m[c][w].v;
+            if (view) view->m[c][w] = V.m[c][w].v;
+            if (proj) proj->m[c][w] = P.m[c][w].v;
+        }
+}
+
 /* :236-237, :261-321 */
 void oracle_reference_objects(float time, rt_object out[5]) {
     float st = time * 0.4f; /* scaled_time = time * time_scale */
     v3 z = V3(0, 0, 0);
     set_obj(&out[0], V3(-11, -11, -11), V3(11, 11, 11), -1.0f, z, z, 6);
-    float s = 0.5f * sinf(st * 0.5f) + 1.5f;
-    set_obj(&out[1], mul3s(V3(-1, -1, -1), s), mul3s(V3(1, 1, 1), s), -1.0f, V3(0, 0, sinf(st * 3.0f)),
+    float s = 0.5f * gv_sincos(st * 0.5f, 0) + 1.5f; /* run-time sin: gallivm */
+    set_obj(&out[1], mul3s(V3(-1, -1, -1), s), mul3s(V3(1, 1, 1), s), -1.0f, V3(0, 0, gv_sincos(st * 3.0f, 0)),
             V3(0, st * 90.0f, 0), 5);
-    set_obj(&out[2], V3(-10, -10, -1), V3(10, 10, 1), -1.0f, V3(0, 0, -3), V3(sinf(st * 5.0f) * 10.0f, 45, 0), 3);
+    set_obj(&out[2], V3(-10, -10, -1), V3(10, 10, 1), -1.0f, V3(0, 0, -3), V3(gv_sincos(st * 5.0f, 0) * 10.0f, 45, 0), 3);
     set_obj(&out[3], V3(-1, -1, -2), V3(1, 1, 2), -1.0f, V3(3, 4, 1),
             V3(45.0f + st * 45.0f, 0, 45.0f + st * 180.0f), 4);
     set_obj(&out[4], z, z, 2.0f, V3(-3, 4, 1), z, 2);
@@ -432,11 +621,11 @@ void oracle_reference_objects(float time, rt_object out[5]) {
 void oracle_reference_camera(float time, rt_camera *c) {
     float radius = 10.0f;
     float speed = time * 0.4f + 0.5f;
-    c->position[0] = radius * cosf(speed);
-    c->position[1] = radius * sinf(speed);
+    c->position[0] = radius * gv_sincos(speed, 1); /* run-time cos / sin: gallivm */
+    c->position[1] = radius * gv_sincos(speed, 0);
     c->position[2] = 0.0f;
     float x = 1.0f * speed * (180.0f / 3.1416f);
-    float yaw = x - 360.0f * floorf(x / 360.0f) + 90.0f; /* GLSL mod */
+    float yaw = (x + 90.0f) - 360.0f * floorf(x / 360.0f); /* GLSL mod + 90, as compiled */
     c->angles[0] = 0.0f; c->angles[1] = yaw; c->angles[2] = 0.0f;
     c->near_plane = 0.1f; c->far_plane = 1000.0f; c->aspect = 16.0f / 9.0f; c->v_fov = 90.0f;
 }
@@ -447,9 +636,14 @@ void oracle_camera_matrices(const rt_camera *cam_in, float time, float out[48]) 
     rt_camera cam;
     if (cam_in) cam = *cam_in;
     else oracle_reference_camera(time, &cam);
-    m4 proj = calc_projection_matrix(&cam);
-    m4 view = calc_view_matrix(&cam);
-    m4 inv = inverse4(mul44(proj, view));
+    m4 proj, view, inv;
+    if (cam_in) {
+        proj = calc_projection_matrix(&cam);
+        view = calc_view_matrix(&cam);
+        inv = inverse4(mul44(proj, view));
+    } else {
+        gl_reference_matrices(time, &inv, &view, &proj);
+    }
     memcpy(out, inv.m, 64);
     memcpy(out + 16, view.m, 64);
     memcpy(out + 32, proj.m, 64);
@@ -753,7 +947,7 @@ int oracle_render_accumulate(const rt_object *objs, int n_objs, const rt_materia
     rt_camera cam;
     if (cam_in) cam = *cam_in;
     else oracle_reference_camera(time, &cam);
-    m4 inv = camera_unprojection(&cam);
+    m4 inv = frame_unprojection(cam_in ? &cam : NULL, time);
     int hw = width / 2, hh = height / 2;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : omp_get_max_threads())
     for (int yy = 0; yy < row1 - row0; yy++) {
@@ -790,7 +984,7 @@ int oracle_render(const rt_object *objs, int n_objs, const rt_material *mats, in
     rt_camera cam;
     if (cam_in) cam = *cam_in;
     else oracle_reference_camera(time, &cam);
-    m4 inv = camera_unprojection(&cam); /* :366-367, :383 */
+    m4 inv = frame_unprojection(cam_in ? &cam : NULL, time); /* :366-367, :383 */
     int hw = width / 2, hh = height / 2;  /* integer halves, :377-378 */
     int nrows = row1 - row0;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : omp_get_max_threads())

@@ -51,6 +51,11 @@ FIXTURES = {
     "config2_1920x1080_cols": ("config2", 1920, 1080, 0, 0.0, (944, 0, 32, 1080), 0),
     "config3_3840x2160_rows": ("config3", 3840, 2160, 2, 0.0, (0, 1076, 3840, 4), 0),
     "config4_7680x4320_crop": ("config4", 7680, 4320, 4, 0.0, (3776, 2112, 128, 16), 0),
+    # the orbit camera moved (t != 0): the product's own camera path
+    # (rt_make_view) against the reference at other camera positions
+    "config2_t1_1920x1080_rows": ("config2", 1920, 1080, 0, 1.0, (0, 300, 1920, 8), 0),
+    "config3_t2.5_3840x2160_rows": ("config3", 3840, 2160, 2, 2.5, (0, 700, 3840, 2), 0),
+    "config4_t7_7680x4320_crop": ("config4", 7680, 4320, 4, 7.0, (2000, 3000, 128, 8), 0),
 }
 
 

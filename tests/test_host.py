@@ -225,3 +225,20 @@ def test_scene_desc_errors_are_reported(text, fragment):
     with pytest.raises(rt.RTError) as e:
         rt.parse_scene(text)
     assert e.value.code == rt.abi.RT_ERR_INVALID and fragment in str(e.value)
+
+
+def test_reference_camera_matches_llvmpipe_golden_vectors():
+    """rt_make_view(NULL, t) — the frame constants rt_render(cam = NULL)
+    uses — equals llvmpipe's inverse(proj_mat * view_mat) (:383) and camera
+    position (:343-344) bit for bit at 600 camera times, negative to 1e4 s
+    (tests/golden/camera_llvmpipe.npz, from the reference's own camera
+    functions: tests/golden/make_camera_golden.py)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "camera_llvmpipe.npz"))
+    for i, t in enumerate(z["time"]):
+        v = rt.make_view(None, float(t))
+        u = np.array(v.unprojection[:], np.float32)
+        o = np.array(v.origin[:], np.float32)
+        assert np.array_equal(u.view(np.uint32), z["unproj"][i].view(np.uint32)), float(t)
+        assert np.array_equal(o.view(np.uint32), z["position"][i].view(np.uint32)), float(t)
+        cam = rt.reference_camera(float(t))
+        assert np.array_equal(np.array(cam.position[:], np.float32), o)
