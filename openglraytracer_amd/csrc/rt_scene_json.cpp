@@ -341,8 +341,18 @@ extern "C" int rt_scene_desc_parse(const char *json, float time, rt_object *objs
                 if (bs->kind != Json::Object) { B.fail("bench_spheres: expected an object"); break; }
                 B.number(bs->get("count"), "count", count);
                 B.number(bs->get("seed"), "seed", seed);
+                // integers in range (a float outside int / uint64 range would
+                // make the conversions undefined)
+                if (!(count >= 0.0f && count <= static_cast<float>(RT_MAX_OBJECTS)) || count != std::floor(count)) {
+                    B.fail("bench_spheres: count must be an integer in [0, " + std::to_string(RT_MAX_OBJECTS) + "]");
+                    break;
+                }
+                if (!(seed >= 0.0f && seed < 9007199254740992.0f) || seed != std::floor(seed)) {
+                    B.fail("bench_spheres: seed must be a non-negative integer below 2^53");
+                    break;
+                }
                 const int n = static_cast<int>(count);
-                if (n < 0 || !room_left(n)) { B.fail("objects: too many"); break; }
+                if (!room_left(n)) { B.fail("objects: too many"); break; }
                 std::vector<rt_object> tmp(static_cast<size_t>(n) + 1);
                 rt_bench_objects(n, static_cast<uint64_t>(seed), tmp.data());
                 for (int i = 0; i < n; ++i) objs[no++] = tmp[static_cast<size_t>(i) + 1];

@@ -216,7 +216,11 @@ def test_scene_desc_explicit_tables_and_camera():
     ('{"objects": [{"sphere": {"radius": 1}, "material": "nope"}]}', "unknown material"),
     ('{"objects": [{"sphere": {"radius": 1}, "material": 7}]}', "out of range"),
     ('{"objects": [{"sphere": {"radius": 1}}]}', "needs a material"),
-    ('{"objects": [{"bench_spheres": {"count": 5000}}]}', "too many"),
+    ('{"objects": [{"bench_spheres": {"count": 5000}}]}', "count must be an integer"),
+    ('{"objects": [{"bench_spheres": {"count": 9e16}}]}', "count must be an integer"),
+    ('{"objects": [{"bench_spheres": {"count": 2.5}}]}', "count must be an integer"),
+    ('{"objects": [{"bench_spheres": {"count": 4, "seed": -1}}]}', "seed must be"),
+    ('{"objects": [{"room": true}, {"bench_spheres": {"count": 1024}}]}', "too many"),
     ('{"lights": [{"position": [1, 2]}]}', "expected 3 numbers"),
     ('[1, 2]', "JSON object"),
     ('{"objects": "reference"} x', "trailing"),
@@ -242,3 +246,17 @@ def test_reference_camera_matches_llvmpipe_golden_vectors():
         assert np.array_equal(o.view(np.uint32), z["position"][i].view(np.uint32)), float(t)
         cam = rt.reference_camera(float(t))
         assert np.array_equal(np.array(cam.position[:], np.float32), o)
+
+
+@pytest.mark.timeout(600)
+def test_host_code_under_address_and_ub_sanitizers():
+    """make asan: the host C++ — scene description parser,
+    scene builder, frame constants, camera, image dump — built with
+    -fsanitize=address,undefined (host only) and driven over the scene files,
+    every truncation of them, seeded mutations and edge cases; any report
+    aborts the run."""
+    import subprocess
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "openglraytracer_amd", "csrc"), "asan"],
+                       capture_output=True, text=True, timeout=580)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "clean" in r.stdout
