@@ -450,11 +450,16 @@ __device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 
     }
 }
 
-// Conservative ray / inflated-box overlap for the BVH: approximate reciprocal
-// direction, slack relative to |t|. The node boxes are inflated on the host
-// by far more than the error of this test, so it never rejects a box whose
-// spheres the exact test could hit; t_max of the node is compared with the
-// running closest t (a sphere's t is at least its box's entry distance).
+// Conservative ray / inflated-box overlap for the BVH. Every node box is
+// its spheres' bounding box grown by m = 1e-3 + 1e-4 |x| (host, rounded
+// outward), so a ray through any point of a sphere's box spends a t-interval
+// of at least m / |d_axis| around it inside the node's slabs. The slab
+// distances here — approximate reciprocal direction, lo * id - o * id as one
+// fma — are off by about 2^-22 |t| + 2^-24 |o| / |d_axis|, under 2e-3 of
+// that margin for origins within 20 units of the centre, so no extra slack
+// is needed: a node whose spheres the exact test could hit before t_limit
+// always passes (tn <= t of the hit < t_limit, tf >= it > 0).
+#ifdef RT_BVH_SLACK
 struct RayInv {
     v3 o, id;
 };
@@ -473,6 +478,26 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
     const float slack = 1e-5f * (fabsf(tn) + fabsf(tf)) + 1e-6f;
     return tn <= tf + slack && tf >= -slack && tn <= t_limit + 1e-5f * fabsf(t_limit) + slack;
 }
+#else
+struct RayInv {
+    v3 oid, id;  // o * id, 1 / d (approximate)
+};
+__device__ __forceinline__ float safe_rcp(float d) {
+    return fabsf(d) > 1e-30f ? __builtin_amdgcn_rcpf(d) : (__float_as_uint(d) >> 31 ? -1e30f : 1e30f);
+}
+__device__ __forceinline__ RayInv ray_inv(const Ray &r) {
+    const v3 id = mk(safe_rcp(r.dir.x), safe_rcp(r.dir.y), safe_rcp(r.dir.z));
+    return {mk(r.start.x * id.x, r.start.y * id.y, r.start.z * id.z), id};
+}
+__device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, float t_limit) {
+    const float x0 = __builtin_fmaf(lo.x, q.id.x, -q.oid.x), x1 = __builtin_fmaf(hi.x, q.id.x, -q.oid.x);
+    const float y0 = __builtin_fmaf(lo.y, q.id.y, -q.oid.y), y1 = __builtin_fmaf(hi.y, q.id.y, -q.oid.y);
+    const float z0 = __builtin_fmaf(lo.z, q.id.z, -q.oid.z), z1 = __builtin_fmaf(hi.z, q.id.z, -q.oid.z);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    return tn <= tf && tf >= 0.0f && tn <= t_limit;
+}
+#endif
 
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>

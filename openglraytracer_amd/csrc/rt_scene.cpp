@@ -383,7 +383,10 @@ void set_skips(std::vector<BvhNode> &nodes, int id, int next) {
     set_skips(nodes, right, next);
 }
 
-void build_bvh(std::vector<SphereRec> &sph, std::vector<SphereMeta> &smeta, std::vector<BvhNode> &nodes) {
+// extent: a bound on |coordinate| of every finite object of the scene (the
+// origins of the secondary rays that walk the BVH lie on their surfaces).
+void build_bvh(std::vector<SphereRec> &sph, std::vector<SphereMeta> &smeta, std::vector<BvhNode> &nodes,
+               double extent) {
     std::vector<BuildItem> finite, other;
     for (size_t i = 0; i < sph.size(); ++i) {
         BuildItem it{sph[i], smeta[i], {}, {}, {}};
@@ -395,7 +398,10 @@ void build_bvh(std::vector<SphereRec> &sph, std::vector<SphereMeta> &smeta, std:
             ok = ok && std::isfinite(c[a]);
             mag = std::max(mag, std::fabs(c[a]) + r);
         }
-        const double margin = 1e-3 + 1e-4 * mag;
+        // the kernel's node test (rt_kernel.hip, node_hit) has no slack of
+        // its own: its error, ~2^-22 (|x| + |o|) / |d|, stays far below this
+        // margin for every box coordinate x and ray origin o of the scene
+        const double margin = 1e-3 + 1e-4 * std::max(mag, extent);
         for (int a = 0; a < 3; ++a) {
             it.c[a] = c[a];
             it.lo[a] = c[a] - r - margin;
@@ -666,8 +672,21 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             boxes.push_back(b);
         }
     }
+    double extent = 0.0;  // |coordinate| bound of the finite objects (BVH margins)
+    for (int i = 0; i < n_objs; ++i) {
+        const rt_object &o = objs[i];
+        double e = std::sqrt(static_cast<double>(o.position[0]) * o.position[0] +
+                             static_cast<double>(o.position[1]) * o.position[1] +
+                             static_cast<double>(o.position[2]) * o.position[2]);
+        double corner = std::fabs(static_cast<double>(o.radius));
+        for (int a = 0; a < 3; ++a)
+            corner = std::max(corner, std::max(std::fabs(static_cast<double>(o.box_mins[a])),
+                                               std::fabs(static_cast<double>(o.box_maxs[a]))));
+        e += corner * std::sqrt(3.0);
+        if (std::isfinite(e)) extent = std::max(extent, e);
+    }
     std::vector<BvhNode> bvh;
-    build_bvh(sph, smeta, bvh);
+    build_bvh(sph, smeta, bvh, extent);
     std::vector<MatRec> mrec(n_mats);
     std::vector<LightMatRec> lm(static_cast<size_t>(n_mats) * n_lights);
     for (int m = 0; m < n_mats; ++m) {
