@@ -548,6 +548,34 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         // secondary rays: stackless depth-first BVH walk (skip links)
         const RayInv q = ray_inv(r);
         int node = valid ? 0 : -1;
+#ifndef RT_BVH_INLINE_LEAVES
+        // while-while: each lane walks nodes until it holds a leaf (or its
+        // walk ends); then the wave tests the spheres of every held leaf
+        // together, so the sphere tests of lanes that reach leaves on
+        // different iterations do not each cost the whole wave a pass
+        int held = 0;  // (count << 24) | first sphere of the held leaf
+        while (__any(node >= 0)) {
+            while (node >= 0 && held == 0) {
+                RT_STAT(3, true);
+                RT_STAT(4, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
+                const float4 lo = S.bvh[2 * node], hi = S.bvh[2 * node + 1];
+                const int leaf = __float_as_int(hi.w);
+                const int skip = __float_as_int(lo.w);
+                if (node_hit(q, lo, hi, h.t)) {
+                    held = leaf;
+                    node = leaf ? skip : node + 1;
+                } else {
+                    node = skip;
+                }
+            }
+            if (held) {
+                RT_STAT(5, true);
+                const int first = held & 0xFFFFFF, count = held >> 24;
+                for (int s = first; s < first + count; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, floor, false, h);
+                held = 0;
+            }
+        }
+#else
         while (node >= 0) {
             RT_STAT(3, true);
             RT_STAT(4, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
@@ -567,6 +595,7 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
                 node = __float_as_int(lo.w);
             }
         }
+#endif
     } else {
         for (int s = 0; s < S.ns; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, floor, kPrimary, h);
     }
