@@ -673,10 +673,20 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         // words are read one at a time, each walked like the LDS masks below
         const int texel = static_cast<int>(static_cast<int64_t>(mask));
         const int per_light = 6 * kGMaskTexels * kGMaskTexels;
-        for (int w = 0; w < S.gwords; ++w) {
+        // every word of the texel requested up front (independent L2 loads
+        // in flight together), then walked word by word
+        constexpr int kMaxWords = kGMaskMaxSpheres / 64;
+        uint64_t words[kMaxWords];
+        const uint64_t *row = S.gmask + (static_cast<size_t>(slot) * per_light + (texel >= 0 ? texel : 0)) * S.gwords;
+#pragma unroll
+        for (int w = 0; w < kMaxWords; ++w)
+            words[w] = (w < S.gwords && need && !hit && texel >= 0) ? row[w] : ~uint64_t{0};
+#pragma unroll
+        for (int w = 0; w < kMaxWords; ++w) {
+            if (w >= S.gwords) break;
             uint64_t cand = 0u;
             if (need && !hit) {
-                cand = texel >= 0 ? S.gmask[(static_cast<size_t>(slot) * per_light + texel) * S.gwords + w] : ~uint64_t{0};
+                cand = words[w];
                 const int rest = S.ns - 64 * w;
                 if (rest < 64) cand &= (uint64_t{1} << rest) - 1u;
             }
