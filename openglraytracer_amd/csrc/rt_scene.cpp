@@ -569,8 +569,12 @@ static void build_direction_masks(const std::vector<SphereRec> &sph, const std::
     };
     for (int j = 0; j < n_lights; ++j) {
         if (lrec[j].dead != 0.0f) continue;
-        // each sphere's cone from this light: axis, half-angle (or everywhere)
-        std::vector<double> ax(3 * sph.size()), half(sph.size());
+        // each sphere's cone from this light: axis, half-angle (or everywhere);
+        // the texel test angle(w, axis) <= alpha + half + 1e-3 is evaluated on
+        // cosines, dot(w, axis) >= cos(alpha + half + 1e-3) (both angles are
+        // below pi; acos is decreasing), with cos / sin of half + 1e-3 per
+        // sphere and of alpha per texel: no inverse cosine per (texel, sphere)
+        std::vector<double> ax(3 * sph.size()), half(sph.size()), ch(sph.size()), sh(sph.size());
         std::vector<char> every(sph.size(), 0);
         for (size_t s = 0; s < sph.size(); ++s) {
             double v[3] = {double(sph[s].cx) - lights[j].position[0], double(sph[s].cy) - lights[j].position[1],
@@ -583,6 +587,8 @@ static void build_direction_masks(const std::vector<SphereRec> &sph, const std::
             }
             for (int k = 0; k < 3; ++k) ax[3 * s + k] = v[k] / d;
             half[s] = std::asin(std::min(1.0, rp / d));
+            ch[s] = std::cos(half[s] + 1e-3);
+            sh[s] = std::sin(half[s] + 1e-3);
         }
         for (int f = 0; f < 6; ++f) {
             const int m = f >> 1, a = m == 0 ? 1 : 0, b = m == 2 ? 1 : 2;
@@ -607,9 +613,13 @@ static void build_direction_masks(const std::vector<SphereRec> &sph, const std::
                     }
                     const size_t at = out.size();
                     out.resize(at + words, 0u);
-                    for (size_t s = 0; s < sph.size(); ++s)
-                        if (every[s] || angle(w, &ax[3 * s]) <= alpha + half[s] + 1e-3)
-                            out[at + s / 64] |= uint64_t{1} << (s % 64);
+                    const double ca = std::cos(alpha), sa = std::sin(alpha);
+                    for (size_t s = 0; s < sph.size(); ++s) {
+                        // cos(alpha + half + 1e-3), less 1e-12 for rounding (far below the 1e-3 rad margin)
+                        const double lim = ca * ch[s] - sa * sh[s] - 1e-12;
+                        const double c = w[0] * ax[3 * s] + w[1] * ax[3 * s + 1] + w[2] * ax[3 * s + 2];
+                        if (every[s] || c >= lim) out[at + s / 64] |= uint64_t{1} << (s % 64);
+                    }
                 }
         }
     }

@@ -1,0 +1,36 @@
+// Host cost of building a scene (rt_scene_create / rt_scene_update minus the
+// upload): make -C openglraytracer_amd/csrc scene-build-time. Prints the
+// median build time of the benchmark scenes (masks, BVH, blob).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <vector>
+
+#include "../../openglraytracer_amd/csrc/rt_internal.h"
+
+namespace rtamd {
+int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
+                int n_lights, std::vector<float4> &blob, DeviceScene &ds);
+}
+
+int main() {
+    rt_material mats[RT_REFERENCE_MATERIALS];
+    rt_light lights[RT_REFERENCE_LIGHTS];
+    rt_reference_materials(mats);
+    rt_reference_lights(lights);
+    for (int n : {16, 64, 256}) {
+        std::vector<rt_object> objs(n + 1);
+        rt_bench_objects(n, 0, objs.data());
+        std::vector<double> ms;
+        for (int rep = 0; rep < 7; ++rep) {
+            std::vector<float4> blob;
+            rtamd::DeviceScene ds;
+            const auto t0 = std::chrono::steady_clock::now();
+            rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds);
+            ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+        std::sort(ms.begin(), ms.end());
+        std::printf("room + %3d spheres: scene build %.3f ms (median of 7)\n", n, ms[3]);
+    }
+    return 0;
+}
