@@ -35,6 +35,7 @@ def load(name):
     L.rt_scene_destroy.argtypes = [vp]
     L.rt_context_set.argtypes = [vp, i, i]
     L.rt_render_view.argtypes = [vp, vp, vp, i, i, i, i, i, vp, i, vp]
+    L.rt_render_batch.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, vp, vp]
     ctx = C.c_void_p()
     assert L.rt_create(0, C.byref(ctx)) == 0
     L.rt_context_set(ctx, rt.abi.RT_OPT_TIMING, 0)
@@ -48,12 +49,15 @@ mats = rt.reference_materials()
 lights = rt.reference_lights()
 view = rt.make_view(None, 0.0)
 for cfg in cfgs:
-    build, w, h, depth = scenes.CONFIGS[cfg]
+    # "<config>x<K>": K animated frames (t = k / 60) per launch (rt_render_batch)
+    batch = int(cfg.split("x")[1]) if "x" in cfg.replace("config", "") else 0
+    build, w, h, depth = scenes.CONFIGS[cfg.split("x")[0]]
+    views = (rt.View * max(batch, 1))(*[rt.make_view(None, k / 60.0) for k in range(max(batch, 1))])
     objs = build()
     oa = (rt.Object * len(objs))(*objs)
     ma = (rt.Material * len(mats))(*mats)
     la = (rt.Light * len(lights))(*lights)
-    out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+    out = torch.empty((max(batch, 1), h, w, 4), dtype=torch.float32, device="cuda")
     reps = 20 if w * h <= 2_100_000 else (4 if w * h <= 8_300_000 else 1)
     state = {}
     for b, (L, ctx) in libs.items():
@@ -65,8 +69,12 @@ for cfg in cfgs:
 
     def launch(b):
         L, ctx = libs[b]
-        rc = L.rt_render_view(ctx, state[b], C.byref(view), w, h, depth, 0, h, C.c_void_p(out.data_ptr()), 1,
-                              C.c_void_p(stream.cuda_stream))
+        if batch:
+            rc = L.rt_render_batch(ctx, state[b], views, batch, w, h, depth, 8, 1, 0, C.c_void_p(out.data_ptr()),
+                                   C.c_void_p(stream.cuda_stream))
+        else:
+            rc = L.rt_render_view(ctx, state[b], C.byref(view), w, h, depth, 0, h, C.c_void_p(out.data_ptr()), 1,
+                                  C.c_void_p(stream.cuda_stream))
         assert rc == 0, rc
 
     for b in builds:  # warm-up + frame hash
@@ -84,7 +92,7 @@ for cfg in cfgs:
             torch.cuda.synchronize()
             times[b].append(e0.elapsed_time(e1) / reps)
     for b in builds:
-        t = np.array(times[b])
+        t = np.array(times[b]) / max(batch, 1)  # per frame
         print("%-8s %-10s median %.4f ms  min %.4f ms  frame %s" % (cfg, b, np.median(t), t.min(), digests[b]),
               flush=True)
     for b, (L, ctx) in libs.items():
