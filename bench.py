@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0,
                     help="approximate budget of the llvmpipe baseline samples")
+    ap.add_argument("--no-single-frame", action="store_true",
+                    help="config2: skip the one-frame-per-launch measurement (profiling runs: one launch shape)")
     return ap.parse_args()
 
 
@@ -374,7 +376,7 @@ def main():
         per_rank = [[round(float(v), 5) for v in e.cpu().tolist()] for e in every]
     else:
         per_rank = [[round(avg_kernel_ms, 5), coll_ms, asm_ms]]
-    if batched and world == 1 and rank == 0:
+    if batched and world == 1 and rank == 0 and not args.no_single_frame:
         # one frame per launch (the shape of the reference's draw(),
         # main.cpp:210-238): K launches back to back, one event pair
         n1 = max(20, args.steps)

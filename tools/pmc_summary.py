@@ -69,7 +69,7 @@ fetch_b = mean(f.get("FETCH_SIZE", [])) * 1024 * 2 if f.get("FETCH_SIZE") else N
 out = {
     "workload": workload, "n_gpus": 1, "frames_per_launch": frames_per_launch, "build": build,
     "kernel_resources": res,
-    "scratch_bytes_per_lane": int(res["Private_Segment_Size"]) if res.get("Private_Segment_Size") else None,
+    "scratch_bytes_per_lane": int(res.get("Scratch_Size") or res.get("Private_Segment_Size") or 0) if res else None,
     "kernel": k[0]["Name"] if k else None,
     "avg_kernel_ns": float(k[0]["AverageNs"]) if k else None, "calls": int(k[0]["Calls"]) if k else None,
     "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
