@@ -631,6 +631,10 @@ __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int b
 
 // Shadow query (:807-819) for the lanes with `need`: is there an object with
 // 0 < t < 1 along start + t * dir? (equivalent to the closest hit's t < 1).
+// Tried and measured no gain (r02, tools/ab.py): dropping the lane's own
+// sphere from its mask when the segment provably leads away from it (config
+// 2 +1 %, configs 3-4 +5-6 %: the extra registers spill), and skipping the
+// square root for spheres behind an outside origin (within 0.5 %).
 // p = the shaded point, L = the light. Called with all lanes active.
 __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
                                          uint64_t mask, bool need) {
@@ -970,9 +974,10 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
 // Depth 0 is one ray (trace0). Deeper trees run as an explicit depth-first
 // walk (trace_tree): every loop iteration traces ONE ray per lane — all lanes
 // execute the same closest-hit + shading code whatever their position in
-// their own tree — and per-level frames (partial colour, pending refraction
-// ray, weights) live in registers. Lanes whose tree is finished ride along
-// with valid = false.
+// their own tree — with per-level frames (partial colour, pending refraction
+// ray, weights) indexed by the lane's own level, which the compiler keeps in
+// scratch (48 B per level). Lanes whose tree is finished ride along with
+// valid = false.
 __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
     RT_PHASE(2);
@@ -998,8 +1003,8 @@ struct Frame {
 };
 
 template <int N>
-struct Frames {  // per-level frames; dynamically indexed (the compiler keeps them in scratch,
-                 // measured faster than per-field register selects at depth 2)
+struct Frames {  // per-level frames, indexed by a per-lane level: the compiler keeps them in
+                 // scratch (measured faster than per-field register selects at depth 2)
     Frame f[N];
     __device__ __forceinline__ Frame get(int level) const {
         Frame r = f[0];
@@ -1091,7 +1096,8 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
     return result;
 }
 
-// Wave-uniform tree walk (default). All 64 lanes of a wave visit the nodes
+// Wave-uniform tree walk (RT_TRACE_TREE=trace_tree_u; measured slower, see
+// below). All 64 lanes of a wave visit the nodes
 // of the full binary ray tree (reflection child first, then refraction
 // child, as the stack machine does, :979-1030) in the same depth-first order;
 // a node is visited when some lane's own tree contains it, and the lanes
