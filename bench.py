@@ -9,13 +9,16 @@ frames of 1920x1080 per GPU (--frames-per-gpu, default 8; frame k is the
 reference orbit camera at time k/60 s), rendered up to 8 frames per launch
 (rt_render_batch; SURVEY.md §8(f) row 3 — several frames per launch amortise
 the launch ramp-up and tail). At N=1 the line also carries the one-frame-per-
-launch rate (`single_frame`, the shape of the reference's draw()). On N GPUs a
-step holds N*F frames: every frame is row-tiled across the N ranks in
-interleaved 8-row blocks, each rank renders its blocks of all N*F frames, and
-one RCCL all-to-all over xGMI hands frames [kF, (k+1)F) to rank k (N gathers
-at once), which de-interleaves its rows. The shards travel as packed float3
-(the alpha channel is the constant 0). The exchange of step i runs on its own
-stream beside the render of step i+1 (double-buffered). Weak scaling.
+launch rate (`single_frame`, the shape of the reference's draw()). On N GPUs
+a step holds N*F frames; the frames of the animated loop are independent
+units, so rank k renders frames [kF, (k+1)F) whole, with no data-path
+collective. Weak scaling. --frame-exchange all_to_all instead row-tiles every
+frame across the N ranks in interleaved 8-row blocks, each rank renders its
+blocks of all N*F frames, and one RCCL all-to-all over xGMI hands frames
+[kF, (k+1)F) to rank k (N gathers at once), which de-interleaves its rows;
+the shards travel as packed float3 (the alpha channel is the constant 0), and
+the exchange of step i runs on its own stream beside the render of step i+1
+(double-buffered).
 
 config3 / config4 (3840x2160 / 64 spheres / depth 2, and
 7680x4320 / 256 spheres / depth 4 row-tiled across the GPUs with an RCCL
@@ -80,6 +83,9 @@ def parse():
     ap.add_argument("--frames-per-gpu", type=int, default=8,
                     help="config2: animated frames each GPU renders per step, up to 8 per launch "
                          "(rt_render_batch; SURVEY.md §8(f) row 3)")
+    ap.add_argument("--frame-exchange", choices=["none", "all_to_all"], default="none",
+                    help="config2 at N>1: none = every rank renders whole frames of its own; all_to_all = "
+                         "every frame row-tiled over the ranks and exchanged (frame k gathered to rank k)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -200,13 +206,32 @@ def main():
     wl = args.workload
     mc = wl == "config5"
     batched = wl == "config2"  # N*F frames per step in batched launches
-    channels = 3 if world > 1 and not mc else 4
+    exchange = batched and world > 1 and args.frame_exchange == "all_to_all"
+    sharded = world > 1 and not mc and (exchange or not batched)  # ranks render row-tiles of shared frames
+    channels = 3 if sharded else 4
     bytes_per_pixel = 4 * channels  # the render's store per pixel (algorithmic HBM bytes)
     if channels == 3:
         ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
     extra = {}
 
-    if batched:
+    if batched and not exchange:
+        # N*F frames in flight, frame k = the orbit camera at t = k/60 s;
+        # rank r renders frames [rF, (r+1)F) whole, up to 8 per launch
+        # (rt_render_batch), in place, launches back to back.
+        fpg = args.frames_per_gpu
+        n_frames = fpg
+        views = [rt.make_view(None, frame_time(rank * fpg + k)) for k in range(fpg)]
+        bufs = [torch.zeros(fpg * H * W * 4, dtype=torch.float32, device="cuda")]
+        chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, fpg, rt.abi.RT_MAX_BATCH)]
+        frame_elems = H * W * 4
+        launches_per_step = len(chunks)
+        px_per_launch = W * H * fpg // launches_per_step
+        rays_per_step = world * fpg * W * H
+
+        def render(buf):
+            for j, vs in chunks:
+                rt.render_batch(ctx, scene, buf.data_ptr() + 4 * j * frame_elems, W, H, DEPTH, vs, stream=sh)
+    elif batched:
         # N frames in flight, frame k = the orbit camera at t = k/60 s; every
         # rank renders its interleaved 8-row blocks of all N frames in one
         # launch (rt_render_batch); one all-to-all hands frame k's rows to
@@ -263,11 +288,11 @@ def main():
                 rt.render_shard(ctx, scene, buf.data_ptr(), W, H, DEPTH, BLOCK_ROWS, world, rank, view=view,
                                 stream=sh)
 
-    # Kernel time from HIP events on the render stream. config2 at N=1: a
-    # step is its render launches alone, one event pair brackets the
-    # back-to-back launches of the whole timed region (no markers between
+    # Kernel time from HIP events on the render stream. config2 without an
+    # exchange: a step is its render launches alone, one event pair brackets
+    # the back-to-back launches of the whole timed region (no markers between
     # frames); otherwise a pair brackets every step's render launches.
-    per_launch = not (batched and world == 1)
+    per_launch = not (batched and not exchange)
     kt = Timer(torch, args.steps if per_launch else 1)
     ct = Timer(torch, args.steps)  # collective (exchange / gather / all-reduce) on comm_s
     at = Timer(torch, args.steps)  # frame assembly on comm_s (rank 0 / every rank for the exchange)
@@ -302,7 +327,7 @@ def main():
             if timed:
                 at.stop(it, comm_s)
             return
-        if world == 1 and not per_launch:  # config2, N=1: frames rendered in place, launches back to back
+        if not per_launch:  # config2 without exchange: frames rendered in place, launches back to back
             render(bufs[0])
             return
         slot = it % 2 if world > 1 else 0
@@ -320,7 +345,7 @@ def main():
         src = bufs[slot] if coll_dev == "cuda" else bufs[slot].cpu()
         if timed:
             ct.start(it, comm_s)
-        if batched:
+        if exchange:
             dist.all_to_all_single(recv[slot], src, out_splits, in_splits)  # frames [kF, (k+1)F) -> rank k
             if timed:
                 ct.stop(it, comm_s)
@@ -364,8 +389,8 @@ def main():
     kernel_ms = ([m / launches_per_step for m in kt.ms()] if per_launch else
                  [kt.ms()[0] / (args.steps * launches_per_step)])
     avg_kernel_ms = float(np.mean(kernel_ms))
-    coll_ms = float(np.mean(ct.ms())) if (world > 1 or mc) else 0.0
-    asm_ms = float(np.mean(at.ms())) if (world > 1 or mc) else 0.0
+    coll_ms = float(np.mean(ct.ms())) if (sharded or mc) else 0.0
+    asm_ms = float(np.mean(at.ms())) if (sharded or mc) else 0.0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -404,10 +429,16 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(wl, args.cpu_seconds)
         workload = {"workload": cfg["text"], "width": W, "height": H, "spheres": cfg["spheres"], "max_depth": DEPTH}
-        if batched:
+        if batched and not exchange:
+            workload.update({"frames_per_step": world * fpg, "frames_per_gpu": fpg, "frames_per_launch": fpl,
+                             "output": "float4 frames",
+                             "parallelism": ("whole frames x%d (rank r renders frames [rF, (r+1)F) of the "
+                                             "animated loop), no collective" % world) if world > 1
+                                            else "single GPU"})
+        elif batched:
             workload.update({"frames_per_step": n_frames, "frames_per_gpu": fpg,
                              "frames_per_launch": fpl, "row_block": BLOCK_ROWS,
-                             "output": "float4 frame" if world == 1 else "float3 shards (alpha 0 dropped) exchanged",
+                             "output": "float3 shards (alpha 0 dropped) exchanged",
                              "parallelism": ("row-tiles x%d + RCCL all-to-all frame exchange (frame k gathered to "
                                              "rank k), overlapped with the next render" % world)
                                             if world > 1 else "single GPU"})
@@ -444,7 +475,7 @@ def main():
                                     for r, v in enumerate(per_rank)],
                        "collective": {"config2": "all_to_all_single (N frame gathers at once)",
                                       "config5": "all_reduce of the sample sums"}.get(
-                                          wl, "gather to rank 0") if world > 1 else "none",
+                                          wl, "gather to rank 0") if (sharded or mc) and world > 1 else "none",
                        "note": "HIP events: kernel on the render stream, collective and assembly on the "
                                "collective stream, means over the timed steps"},
             "cpu_baseline": cpu,
