@@ -552,7 +552,12 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         // while-while: each lane walks nodes until it holds a leaf (or its
         // walk ends); then the wave tests the spheres of every held leaf
         // together, so the sphere tests of lanes that reach leaves on
-        // different iterations do not each cost the whole wave a pass
+        // different iterations do not each cost the whole wave a pass.
+        // Tried and measured slower (r02, tools/ab.py; the extra registers
+        // spill at the 80-VGPR cap): reading both successors' records before
+        // the node test (config 4 22.0 -> 24.7 ms, config 3 1.058 -> 1.128 ms);
+        // loading the wide-mask words in phong ahead of the shading math
+        // (22.0 -> 23.6 ms, 1.058 -> 1.149 ms).
         int held = 0;  // (count << 24) | first sphere of the held leaf
         while (__any(node >= 0)) {
             while (node >= 0 && held == 0) {
