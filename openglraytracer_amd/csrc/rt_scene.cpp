@@ -285,7 +285,7 @@ namespace {
 // Build a BVH over the spheres with finite centre and radius (the others can
 // never produce a valid hit: their quadratic is NaN or its roots infinite),
 // reordering `sph`/`smeta` into leaf order. Median split on the widest
-// centroid axis, leaves of <= 4 spheres, depth-first layout with skip links.
+// centroid axis, leaves of <= RT_BVH_LEAF spheres, depth-first layout with skip links.
 struct BuildItem {
     SphereRec s;
     SphereMeta m;
@@ -309,7 +309,10 @@ int build_node(std::vector<BuildItem> &items, int begin, int end, std::vector<Bv
         n.lo[a] = std::nextafter(static_cast<float>(lo[a]), -INFINITY);
         n.hi[a] = std::nextafter(static_cast<float>(hi[a]), INFINITY);
     }
-    if (end - begin <= 4) {
+#ifndef RT_BVH_LEAF  // leaves of up to 6 spheres: config 4 22.04 -> 21.82 ms against 4 (2: 24.7, 3: 22.3, 8: 21.8;
+#define RT_BVH_LEAF 6  // SAH leaf termination at 6-8 spheres: 22.3-29.2 ms); config 3 within 0.5 %
+#endif
+    if (end - begin <= RT_BVH_LEAF) {
         n.leaf = ((end - begin) << 24) | begin;
         return id;
     }
