@@ -110,6 +110,12 @@ struct BvhNode {
     int32_t leaf;
 };
 static_assert(sizeof(BvhNode) == 32, "BvhNode layout");
+// Ordered traversal of the closest-hit walk: per node, 8 link words, one per
+// ray-direction octant (bit a set: d[a] < 0), each (next node on a hit) |
+// (next node on a miss) << 16, 0xFFFF = end. The octant's depth-first order
+// enters every inner node's children nearer-first along its split axis, so
+// near hits shrink the search interval before the far subtree is tested.
+constexpr int kBvhOctants = 8;
 
 struct LightRec {
     float pos[3];
@@ -143,6 +149,7 @@ struct LaunchParams {
     float4 *out;        // n_views x n_rows x width float4
     int32_t off_spheres, off_smeta, off_boxes, off_mats, off_lights, off_lightmat;  // 16-B units
     int32_t off_bvh, n_bvh;  // sphere BVH nodes (2 x float4 each), 16-B units / count
+    int32_t off_blink;       // n_bvh x kBvhOctants uint32 traversal links, 16-B units
     int32_t off_cone;        // n_lights x n_spheres ShadowCone, 16-B units; -1: none
                              // (kept only while the LDS total stays within kConeLdsBudget)
     int32_t off_dmask, dmask_n;  // shadow direction masks (live lights x 6 x n x n), 16-B units; -1: none
@@ -181,7 +188,7 @@ struct DeviceScene {
     void *blob = nullptr;
     int32_t blob_units = 0;
     int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
-    int32_t off_bvh = 0, n_bvh = 0, off_cone = 0;
+    int32_t off_bvh = 0, n_bvh = 0, off_blink = 0, off_cone = 0;
     int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
     int32_t off_gmask = -1, gmask_words = 0;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;

@@ -241,6 +241,7 @@ struct Scene {
     const LightRec *light;
     const LightMatRec *lm;
     const float4 *bvh;  // BvhNode pairs (lo, hi)
+    const uint32_t *blink;  // per node, kBvhOctants traversal links
     const ShadowCone *cone;  // [light][sphere] shadow culling cones
     const char *dmask;  // [live light][face][row][col] shadow direction masks (nullptr: none)
     int dmask_n, dmask_bytes;
@@ -559,12 +560,25 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         // loading the wide-mask words in phong ahead of the shading math
         // (22.0 -> 23.6 ms, 1.058 -> 1.149 ms).
         int held = 0;  // (count << 24) | first sphere of the held leaf
+#ifndef RT_BVH_FIXED
+        // the ray's octant picks its traversal order (nearer child first)
+        const int oct = (r.dir.x < 0.0f ? 1 : 0) | (r.dir.y < 0.0f ? 2 : 0) | (r.dir.z < 0.0f ? 4 : 0);
+#endif
         while (__any(node >= 0)) {
             while (node >= 0 && held == 0) {
                 RT_STAT(3, true);
                 RT_STAT(4, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 const float4 lo = S.bvh[2 * node], hi = S.bvh[2 * node + 1];
                 const int leaf = __float_as_int(hi.w);
+#ifndef RT_BVH_FIXED
+                const uint32_t link = S.blink[node * kBvhOctants + oct];
+                if (node_hit(q, lo, hi, h.t)) {
+                    held = leaf;
+                    node = static_cast<int16_t>(link & 0xFFFFu);
+                } else {
+                    node = static_cast<int16_t>(link >> 16);
+                }
+#else
                 const int skip = __float_as_int(lo.w);
                 if (node_hit(q, lo, hi, h.t)) {
                     held = leaf;
@@ -572,6 +586,7 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
                 } else {
                     node = skip;
                 }
+#endif
             }
             if (held) {
                 RT_STAT(5, true);
@@ -1559,6 +1574,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.light = reinterpret_cast<const LightRec *>(lds + p.off_lights);
     S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
     S.bvh = lds + p.off_bvh;
+    S.blink = reinterpret_cast<const uint32_t *>(lds + p.off_blink);
     S.cone = p.off_cone >= 0 ? reinterpret_cast<const ShadowCone *>(lds + p.off_cone) : nullptr;
     S.dmask = p.off_dmask >= 0 ? reinterpret_cast<const char *>(lds + p.off_dmask) : nullptr;
     S.dmask_n = p.dmask_n;

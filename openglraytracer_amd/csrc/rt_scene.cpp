@@ -292,9 +292,11 @@ struct BuildItem {
     double lo[3], hi[3], c[3];
 };
 
-int build_node(std::vector<BuildItem> &items, int begin, int end, std::vector<BvhNode> &nodes) {
+int build_node(std::vector<BuildItem> &items, int begin, int end, std::vector<BvhNode> &nodes,
+               std::vector<int> &axes) {
     const int id = static_cast<int>(nodes.size());
     nodes.push_back(BvhNode{});
+    axes.push_back(0);
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     double clo[3] = {1e300, 1e300, 1e300}, chi[3] = {-1e300, -1e300, -1e300};
     for (int i = begin; i < end; ++i)
@@ -364,8 +366,9 @@ int build_node(std::vector<BuildItem> &items, int begin, int end, std::vector<Bv
     std::sort(items.begin() + begin, items.begin() + end,
               [axis](const BuildItem &x, const BuildItem &y) { return x.c[axis] < y.c[axis]; });
     nodes[id].leaf = 0;
-    build_node(items, begin, mid, nodes);
-    build_node(items, mid, end, nodes);
+    axes[id] = axis;
+    build_node(items, begin, mid, nodes, axes);
+    build_node(items, mid, end, nodes, axes);
     return id;
 }
 
@@ -386,10 +389,29 @@ void set_skips(std::vector<BvhNode> &nodes, int id, int next) {
     set_skips(nodes, right, next);
 }
 
+// The octant's depth-first order (rt_internal.h, kBvhOctants): the children
+// of an inner node split on axis a (left: the lower centroids) are entered
+// right first when the octant's d[a] < 0.
+static_assert(2 * RT_MAX_OBJECTS < 0x8000, "BVH node indices fit the 16-bit links");
+void set_links(const std::vector<BvhNode> &nodes, const std::vector<int> &axes, int id, int next, int oct,
+               std::vector<uint32_t> &links) {
+    auto enc = [](int n) { return static_cast<uint32_t>(n) & 0xFFFFu; };  // -1 -> 0xFFFF
+    if (nodes[id].leaf) {
+        links[static_cast<size_t>(id) * kBvhOctants + oct] = enc(next) | (enc(next) << 16);
+        return;
+    }
+    const int left = id + 1, right = left + subtree_size(nodes, left);
+    const bool flip = (oct >> axes[id]) & 1;
+    const int first = flip ? right : left, second = flip ? left : right;
+    links[static_cast<size_t>(id) * kBvhOctants + oct] = enc(first) | (enc(next) << 16);
+    set_links(nodes, axes, first, second, oct, links);
+    set_links(nodes, axes, second, next, oct, links);
+}
+
 // extent: a bound on |coordinate| of every finite object of the scene (the
 // origins of the secondary rays that walk the BVH lie on their surfaces).
 void build_bvh(std::vector<SphereRec> &sph, std::vector<SphereMeta> &smeta, std::vector<BvhNode> &nodes,
-               double extent) {
+               std::vector<uint32_t> &links, double extent) {
     std::vector<BuildItem> finite, other;
     for (size_t i = 0; i < sph.size(); ++i) {
         BuildItem it{sph[i], smeta[i], {}, {}, {}};
@@ -413,9 +435,13 @@ void build_bvh(std::vector<SphereRec> &sph, std::vector<SphereMeta> &smeta, std:
         (ok ? finite : other).push_back(it);
     }
     nodes.clear();
+    links.clear();
     if (!finite.empty()) {
-        build_node(finite, 0, static_cast<int>(finite.size()), nodes);
+        std::vector<int> axes;
+        build_node(finite, 0, static_cast<int>(finite.size()), nodes, axes);
         set_skips(nodes, 0, -1);
+        links.assign(nodes.size() * kBvhOctants, 0u);
+        for (int oct = 0; oct < kBvhOctants; ++oct) set_links(nodes, axes, 0, -1, oct, links);
     }
     // leaf order first, then the spheres that cannot be hit (linear loops only)
     sph.clear();
@@ -699,7 +725,8 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         if (std::isfinite(e)) extent = std::max(extent, e);
     }
     std::vector<BvhNode> bvh;
-    build_bvh(sph, smeta, bvh, extent);
+    std::vector<uint32_t> blink;
+    build_bvh(sph, smeta, bvh, blink, extent);
     std::vector<MatRec> mrec(n_mats);
     std::vector<LightMatRec> lm(static_cast<size_t>(n_mats) * n_lights);
     for (int m = 0; m < n_mats; ++m) {
@@ -781,6 +808,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     ds.off_lights = off;  off += units(lrec.size() * sizeof(LightRec));
     ds.off_lightmat = off; off += units(lm.size() * sizeof(LightMatRec));
     ds.off_bvh = off;     off += units(bvh.size() * sizeof(BvhNode));
+    ds.off_blink = off;   off += units(blink.size() * sizeof(uint32_t));
     // The cone table rides in LDS only while the work-group's LDS stays small
     // enough for full occupancy (config 4's 256 spheres x 3 lights would add
     // 24 KB and cut the resident work-groups per CU); without it the kernel
@@ -857,6 +885,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     put(ds.off_lights, lrec.data(), lrec.size() * sizeof(LightRec));
     put(ds.off_lightmat, lm.data(), lm.size() * sizeof(LightMatRec));
     put(ds.off_bvh, bvh.data(), bvh.size() * sizeof(BvhNode));
+    put(ds.off_blink, blink.data(), blink.size() * sizeof(uint32_t));
     if (ds.off_cone >= 0) put(ds.off_cone, cones.data(), cones.size() * sizeof(ShadowCone));
     if (ds.off_dmask >= 0) put(ds.off_dmask, dmask_bytes.data(), dmask_bytes.size());
     if (ds.off_gmask >= 0) put(ds.off_gmask, gmask.data(), gmask.size() * 8);
