@@ -1024,20 +1024,12 @@ struct Frame {
 
 template <int N>
 struct Frames {  // per-level frames, indexed by a per-lane level: the compiler keeps them in
-                 // scratch (measured faster than per-field register selects at depth 2)
+                 // scratch; indexed directly, a push or pop moves one 48-B frame (per-level
+                 // selects read every level's frame: config 4 18.80 vs 19.08 ms, depth-4
+                 // scratch 292 vs 400 B per lane)
     Frame f[N];
-    __device__ __forceinline__ Frame get(int level) const {
-        Frame r = f[0];
-#pragma unroll
-        for (int i = 1; i < N; ++i)
-            if (level == i) r = f[i];
-        return r;
-    }
-    __device__ __forceinline__ void set(int level, const Frame &v) {
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            if (level == i) f[i] = v;
-    }
+    __device__ __forceinline__ Frame get(int level) const { return f[level]; }
+    __device__ __forceinline__ void set(int level, const Frame &v) { f[level] = v; }
 };
 
 template <int kDepth>
