@@ -91,10 +91,11 @@ constexpr int kMaskMaxSpheres = 64;
 constexpr size_t kMaskLdsBudget = 19 * 1024;
 // Larger scenes (up to kGMaskMaxSpheres) use the same masks as 64-bit words
 // per texel, kGMaskTexels per face edge, in the device blob after the part
-// the work-groups stage (read through L2: 256 spheres, 192 KB per live light at 32 texels).
+// the work-groups stage (read through L2: 256 spheres, 768 KB per live light at 64 texels).
 constexpr int kGMaskMaxSpheres = 256;
 #ifndef RT_GMASK_TEXELS
-#define RT_GMASK_TEXELS 32  // tuning knob (tools/ablate.sh flags); 8/16/24/32/48/64: config 4 28.2/25.9/25.2/25.0/24.9/24.8 ms
+#define RT_GMASK_TEXELS 64  // tuning knob (tools/ablate.sh flags); 8/16/24/32/48/64: config 4 28.2/25.9/25.2/25.0/24.9/24.8 ms
+                            // (r01); after the ordered BVH 32/48/64: 18.29/17.91/17.73 ms, config 3 1.002/1.005/0.996 ms
 #endif
 constexpr int kGMaskTexels = RT_GMASK_TEXELS;
 // Sphere BVH node (depth-first order; the left child is the next node):

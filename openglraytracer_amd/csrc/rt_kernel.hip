@@ -652,9 +652,10 @@ __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int b
 // Shadow query (:807-819) for the lanes with `need`: is there an object with
 // 0 < t < 1 along start + t * dir? (equivalent to the closest hit's t < 1).
 // Tried and measured no gain (r02, tools/ab.py): dropping the lane's own
-// sphere from its mask when the segment provably leads away from it (config
-// 2 +1 %, configs 3-4 +5-6 %: the extra registers spill), and skipping the
-// square root for spheres behind an outside origin (within 0.5 %).
+// sphere from its mask when the segment provably starts outside it and
+// leads away from it (config 2 +1-4 %, configs 3-4 +6-12 %, also after the
+// frames shrank: the extra registers spill), and skipping the square root
+// for spheres behind an outside origin (within 0.5 %).
 // p = the shaded point, L = the light. Called with all lanes active.
 __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
                                          uint64_t mask, bool need) {
@@ -996,7 +997,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
 // execute the same closest-hit + shading code whatever their position in
 // their own tree — with per-level frames (partial colour, pending refraction
 // ray, weights) indexed by the lane's own level, which the compiler keeps in
-// scratch (48 B per level). Lanes whose tree is finished ride along with
+// scratch (40 B per level). Lanes whose tree is finished ride along with
 // valid = false.
 __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
@@ -1018,13 +1019,14 @@ __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
 struct Frame {
     v3 col;       // phong, then mix(phong, R, rho) once the reflection returned
     v3 rs, rd;    // pending refraction ray (:1010-1023)
-    float rho, tau;
-    int flags;    // 1: refraction spawned; 2: waiting for the reflection; 4: for the refraction
+    int flags;    // 1: refraction spawned; 2: waiting for the reflection; 4: for the refraction;
+                  // | material << 3 (rho and tau read back from it: a 40-B frame instead of
+                  // 48, config 4 18.68 -> 18.26 ms, config 3 1.022 -> 1.000 ms)
 };
 
 template <int N>
 struct Frames {  // per-level frames, indexed by a per-lane level: the compiler keeps them in
-                 // scratch; indexed directly, a push or pop moves one 48-B frame (per-level
+                 // scratch; indexed directly, a push or pop moves one 40-B frame (per-level
                  // selects read every level's frame: config 4 18.80 vs 19.08 ms, depth-4
                  // scratch 292 vs 400 B per lane)
     Frame f[N];
@@ -1060,13 +1062,11 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
         if (sr || st) {  // push this node, descend into its first child
             Frame fr;
             fr.col = col;
-            fr.rho = m.reflectivity;
-            fr.tau = m.transparency;
             fr.rs = sub(c.p, muls(c.n, 0.001f));
             float ratio = 1.0f / m.refraction_index;
             if (c.inside) ratio = 1.0f / ratio;
             fr.rd = refract(ray.dir, c.n, ratio);
-            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4);
+            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3);
             F.set(level, fr);
             if (sr) {
                 ray.start = add(c.p, muls(c.n, 0.001f));
@@ -1083,10 +1083,12 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
         bool next_child = false;
         while (level > 0 && !next_child) {
             Frame fr = F.get(level - 1);
+            const MatRec &fm = S.mat[fr.flags >> 3];
+            const float rho = fm.reflectivity, tau = fm.transparency;
             if (fr.flags & 2) {
-                fr.col = mix(fr.col, value, fr.rho);
+                fr.col = mix(fr.col, value, rho);
                 if (fr.flags & 1) {  // the refraction child comes next
-                    fr.flags = 4;
+                    fr.flags = (fr.flags & ~7) | 4;
                     F.set(level - 1, fr);
                     ray.start = fr.rs;
                     ray.dir = fr.rd;
@@ -1096,7 +1098,7 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
                     --level;
                 }
             } else {
-                value = mix(fr.col, value, fr.tau);
+                value = mix(fr.col, value, tau);
                 --level;
             }
         }

@@ -10,6 +10,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -571,6 +574,95 @@ static void view_frame_setup(const LaunchParams &p, const FrameView &V, const fl
     }
 }
 
+// The texel and block cones of an n x n cube map (geometry only: computed
+// once per n and kept). Texels are grouped in blocks of kMaskBlock x
+// kMaskBlock; a block's reach is its own cone's half-angle plus the largest
+// half-angle of its texels.
+constexpr int kMaskBlock = 8;
+struct MaskCones {
+    int n = 0;
+    std::vector<double> w, ca, sa;  // per texel (face-major): centre direction, cos / sin of the half-angle
+    struct Block {
+        int face, r0, r1, c0, c1;
+        double w[3], reach, cr, sr;  // centre direction, reach and its cos / sin
+    };
+    std::vector<Block> blocks;
+};
+
+const MaskCones &mask_cones(int n) {
+    static std::mutex mu;
+    static std::map<int, std::unique_ptr<MaskCones>> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    std::unique_ptr<MaskCones> &slot = cache[n];
+    if (slot) return *slot;
+    auto unit = [](double v[3]) {
+        const double l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        for (int k = 0; k < 3; ++k) v[k] /= l;
+    };
+    auto angle = [](const double a[3], const double b[3]) {
+        const double c = a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+        return std::acos(std::max(-1.0, std::min(1.0, c)));
+    };
+    auto mc = std::make_unique<MaskCones>();
+    mc->n = n;
+    const size_t texels = static_cast<size_t>(6) * n * n;
+    mc->w.resize(3 * texels);
+    mc->ca.resize(texels);
+    mc->sa.resize(texels);
+    std::vector<double> alpha(texels);
+    for (int f = 0; f < 6; ++f) {
+        const int m = f >> 1, a = m == 0 ? 1 : 0, b = m == 2 ? 1 : 2;
+        const double sg = (f & 1) ? -1.0 : 1.0;
+        // a square [a0, a1] x [b0, b1] of the face: its centre direction and
+        // the half-angle of the cone through its corners
+        auto cone = [&](double a0, double a1, double b0, double b1, double w[3]) {
+            w[m] = sg;
+            w[a] = 0.5 * (a0 + a1);
+            w[b] = 0.5 * (b0 + b1);
+            unit(w);
+            double al = 0.0;
+            for (int k = 0; k < 4; ++k) {
+                double q[3];
+                q[m] = sg;
+                q[a] = (k & 1) ? a1 : a0;
+                q[b] = (k & 2) ? b1 : b0;
+                unit(q);
+                al = std::max(al, angle(w, q));
+            }
+            return al;
+        };
+        for (int row = 0; row < n; ++row)
+            for (int col = 0; col < n; ++col) {
+                const size_t t = (static_cast<size_t>(f) * n + row) * n + col;
+                alpha[t] = cone(-1.0 + 2.0 * col / n, -1.0 + 2.0 * (col + 1) / n, -1.0 + 2.0 * row / n,
+                                -1.0 + 2.0 * (row + 1) / n, &mc->w[3 * t]);
+                mc->ca[t] = std::cos(alpha[t]);
+                mc->sa[t] = std::sin(alpha[t]);
+            }
+        for (int r0 = 0; r0 < n; r0 += kMaskBlock)
+            for (int c0 = 0; c0 < n; c0 += kMaskBlock) {
+                MaskCones::Block bl;
+                bl.face = f;
+                bl.r0 = r0;
+                bl.c0 = c0;
+                bl.r1 = std::min(n, r0 + kMaskBlock);
+                bl.c1 = std::min(n, c0 + kMaskBlock);
+                bl.reach = cone(-1.0 + 2.0 * bl.c0 / n, -1.0 + 2.0 * bl.c1 / n, -1.0 + 2.0 * bl.r0 / n,
+                                -1.0 + 2.0 * bl.r1 / n, bl.w);
+                double amax = 0.0;
+                for (int row = bl.r0; row < bl.r1; ++row)
+                    for (int col = bl.c0; col < bl.c1; ++col)
+                        amax = std::max(amax, alpha[(static_cast<size_t>(f) * n + row) * n + col]);
+                bl.reach += amax;
+                bl.cr = std::cos(bl.reach);
+                bl.sr = std::sin(bl.reach);
+                mc->blocks.push_back(bl);
+            }
+    }
+    slot = std::move(mc);
+    return *slot;
+}
+
 // Build the device blob: [spheres][sphere meta][boxes][materials][lights]
 // [light x material products]; every section 16-B aligned.
 // Shadow direction masks (rt_internal.h, kMaskMaxSpheres): float64 geometry.
@@ -583,19 +675,16 @@ static void view_frame_setup(const LaunchParams &p, const FrameView &V, const fl
 // of the cube face; it lies inside the cone around its centre direction
 // whose half-angle is the largest angle to its four corners (a cone narrower
 // than 90 degrees is convex, so holding the corners it holds the square).
+// Spheres are tested texel by texel only in the blocks whose reach their
+// cone comes within (a texel's centre lies in its block's cone, so every
+// texel the texel test accepts lies in an accepted block): the bits set are
+// those of the texel-by-texel test alone.
 static void build_direction_masks(const std::vector<SphereRec> &sph, const std::vector<SphereMeta> &smeta,
                            const rt_light *lights, const std::vector<LightRec> &lrec, int n,
                            std::vector<uint64_t> &out, int words = 1) {
     const int n_lights = static_cast<int>(lrec.size());
+    const MaskCones &mc = mask_cones(n);
     out.clear();
-    auto unit = [](double v[3]) {
-        const double l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-        for (int k = 0; k < 3; ++k) v[k] /= l;
-    };
-    auto angle = [](const double a[3], const double b[3]) {
-        const double c = a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
-        return std::acos(std::max(-1.0, std::min(1.0, c)));
-    };
     for (int j = 0; j < n_lights; ++j) {
         if (lrec[j].dead != 0.0f) continue;
         // each sphere's cone from this light: axis, half-angle (or everywhere);
@@ -619,38 +708,26 @@ static void build_direction_masks(const std::vector<SphereRec> &sph, const std::
             ch[s] = std::cos(half[s] + 1e-3);
             sh[s] = std::sin(half[s] + 1e-3);
         }
-        for (int f = 0; f < 6; ++f) {
-            const int m = f >> 1, a = m == 0 ? 1 : 0, b = m == 2 ? 1 : 2;
-            const double sg = (f & 1) ? -1.0 : 1.0;
-            for (int row = 0; row < n; ++row)
-                for (int col = 0; col < n; ++col) {
-                    const double a0 = -1.0 + 2.0 * col / n, a1 = -1.0 + 2.0 * (col + 1) / n;
-                    const double b0 = -1.0 + 2.0 * row / n, b1 = -1.0 + 2.0 * (row + 1) / n;
-                    double w[3];
-                    w[m] = sg;
-                    w[a] = 0.5 * (a0 + a1);
-                    w[b] = 0.5 * (b0 + b1);
-                    unit(w);
-                    double alpha = 0.0;
-                    for (int k = 0; k < 4; ++k) {
-                        double q[3];
-                        q[m] = sg;
-                        q[a] = (k & 1) ? a1 : a0;
-                        q[b] = (k & 2) ? b1 : b0;
-                        unit(q);
-                        alpha = std::max(alpha, angle(w, q));
-                    }
-                    const size_t at = out.size();
-                    out.resize(at + words, 0u);
-                    const double ca = std::cos(alpha), sa = std::sin(alpha);
-                    for (size_t s = 0; s < sph.size(); ++s) {
-                        // cos(alpha + half + 1e-3), less 1e-12 for rounding (far below the 1e-3 rad margin)
-                        const double lim = ca * ch[s] - sa * sh[s] - 1e-12;
-                        const double c = w[0] * ax[3 * s] + w[1] * ax[3 * s + 1] + w[2] * ax[3 * s + 2];
-                        if (every[s] || c >= lim) out[at + s / 64] |= uint64_t{1} << (s % 64);
-                    }
+        const size_t base = out.size();
+        out.resize(base + static_cast<size_t>(6) * n * n * words, 0u);
+        for (const MaskCones::Block &bl : mc.blocks)
+            for (size_t s = 0; s < sph.size(); ++s) {
+                if (!every[s]) {
+                    // cos(reach + half + 1e-3), less a margin for rounding
+                    const double lim = bl.cr * ch[s] - bl.sr * sh[s] - 1e-9;
+                    const double c = bl.w[0] * ax[3 * s] + bl.w[1] * ax[3 * s + 1] + bl.w[2] * ax[3 * s + 2];
+                    if (bl.reach + half[s] + 1e-3 < 3.141592653589793 && c < lim) continue;
                 }
-        }
+                for (int row = bl.r0; row < bl.r1; ++row)
+                    for (int col = bl.c0; col < bl.c1; ++col) {
+                        const size_t t = (static_cast<size_t>(bl.face) * n + row) * n + col;
+                        const double *w = &mc.w[3 * t];
+                        // cos(alpha + half + 1e-3), less 1e-12 for rounding (far below the 1e-3 rad margin)
+                        const double lim = mc.ca[t] * ch[s] - mc.sa[t] * sh[s] - 1e-12;
+                        const double c = w[0] * ax[3 * s] + w[1] * ax[3 * s + 1] + w[2] * ax[3 * s + 2];
+                        if (every[s] || c >= lim) out[base + t * words + s / 64] |= uint64_t{1} << (s % 64);
+                    }
+            }
     }
 }
 

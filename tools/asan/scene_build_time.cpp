@@ -1,9 +1,12 @@
 // Host cost of building a scene (rt_scene_create / rt_scene_update minus the
 // upload): make -C openglraytracer_amd/csrc scene-build-time. Prints the
-// median build time of the benchmark scenes (masks, BVH, blob).
+// median build time of the benchmark scenes (masks, BVH, blob) and a hash of
+// each blob (builder changes that must not change the scene compare it).
 #include <algorithm>
 #include <chrono>
+#include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "../../openglraytracer_amd/csrc/rt_internal.h"
@@ -18,19 +21,25 @@ int main() {
     rt_light lights[RT_REFERENCE_LIGHTS];
     rt_reference_materials(mats);
     rt_reference_lights(lights);
-    for (int n : {16, 64, 256}) {
+    for (int n : {16, 33, 64, 100, 256}) {
         std::vector<rt_object> objs(n + 1);
         rt_bench_objects(n, 0, objs.data());
         std::vector<double> ms;
+        uint64_t hash = 1469598103934665603ull;  // FNV-1a over the blob bytes
         for (int rep = 0; rep < 7; ++rep) {
             std::vector<float4> blob;
             rtamd::DeviceScene ds;
             const auto t0 = std::chrono::steady_clock::now();
             rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds);
             ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+            if (rep == 0) {
+                const unsigned char *b = reinterpret_cast<const unsigned char *>(blob.data());
+                for (size_t i = 0; i < blob.size() * sizeof(float4); ++i) hash = (hash ^ b[i]) * 1099511628211ull;
+            }
         }
         std::sort(ms.begin(), ms.end());
-        std::printf("room + %3d spheres: scene build %.3f ms (median of 7)\n", n, ms[3]);
+        std::printf("room + %3d spheres: scene build %.3f ms (median of 7), blob %016llx\n", n, ms[3],
+                    static_cast<unsigned long long>(hash));
     }
     return 0;
 }
