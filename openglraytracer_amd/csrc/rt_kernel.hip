@@ -655,7 +655,9 @@ __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int b
 // sphere from its mask when the segment provably starts outside it and
 // leads away from it (config 2 +1-4 %, configs 3-4 +6-12 %, also after the
 // frames shrank: the extra registers spill), and skipping the square root
-// for spheres behind an outside origin (within 0.5 %).
+// for spheres behind an outside origin (within 0.5 %), also as a separate
+// first pass over the LDS mask that drops such candidates before the exact
+// walk (config 2 even).
 // p = the shaded point, L = the light. Called with all lanes active.
 __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
                                          uint64_t mask, bool need) {
