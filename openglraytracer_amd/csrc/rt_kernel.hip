@@ -1501,7 +1501,10 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 // Queued distribution pays where the cost per wave tile varies most (the
 // recursive depths); depth 0 / 1 keep the tiled kernel, whose body the
 // compiler schedules with fewer registers (config 2: 70 vs 81 VGPRs).
-constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
+#ifndef RT_QUEUED_MIN_DEPTH  // r02: queued from depth 0 (64 VGPRs + 84 B scratch): config 2 single frame
+#define RT_QUEUED_MIN_DEPTH 2  // 52 -> 67 us, 8-frame launches (tiled either way) 41.5 -> 50.6 us per frame
+#endif
+constexpr bool kQueuedDepth(int depth) { return depth >= RT_QUEUED_MIN_DEPTH; }
 
 template <int kDepth, bool kAccum>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
