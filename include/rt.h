@@ -133,6 +133,14 @@ int rt_bench_objects(int n_spheres, uint64_t seed, rt_object *out);
 /* cam == NULL: the reference orbit camera at `time`. */
 int rt_make_view(const rt_camera *cam, float time, rt_view *out);
 
+/* The transforms a box object is intersected with, as the reference's GL
+ * evaluates them per ray (raytrace_compute.glsl:650-652, :718, replacing
+ * calc_transform_matrix / inverse / transpose(inverse(mat3(.)))):
+ * local_to_world and world_to_local (column-major 4x4, m[col][row] at
+ * col * 4 + row) and the normal matrix (column-major 3x3). The scene builder
+ * stores exactly these; exposed for tests and tools. */
+int rt_object_transforms(const rt_object *obj, float l2w[16], float w2l[16], float nrm[9]);
+
 /* Scene description input: the content the reference
  * compiles into its shader (materials :74-157, lights :199-224, the animated
  * objects :261-321 at `time`, the camera :334-364) read from JSON text —

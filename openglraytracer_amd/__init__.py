@@ -57,6 +57,7 @@ def lib():
             "rt_reference_materials": ([vp], i), "rt_reference_lights": ([vp], i),
             "rt_reference_objects": ([f, vp], i), "rt_reference_camera": ([f, vp], i),
             "rt_bench_objects": ([i, C.c_uint64, vp], i), "rt_make_view": ([vp, f, vp], i),
+            "rt_object_transforms": ([vp, vp, vp, vp], i),
             "rt_create": ([i, vp], i), "rt_destroy": ([vp], None),
             "rt_scene_create": ([vp, vp, i, vp, i, vp, i, vp], i), "rt_scene_destroy": ([vp], None),
             "rt_scene_update": ([vp, vp, vp, i, vp, i, vp, i], i),

@@ -217,6 +217,36 @@ Gm inverse(const Gm &M) {
     return r;
 }
 
+// transpose(inverse(mat3(m))) as Mesa's builtin lowers inverse(mat3): the
+// three cofactors of the first column, det = (m00 c0 - m01 c1) + m02 c2, the
+// adjugate over det; returned column-major (r[col][row]).
+void normal_matrix(const Gm &M, Gf r[3][3]) {
+    const Gf(*m)[4] = M.m;
+    auto d = [](const Gf &a, const Gf &b, const Gf &c, const Gf &e) { return sub(mul(a, b), mul(c, e)); };
+    const Gf f0 = d(m[1][1], m[2][2], m[2][1], m[1][2]);
+    const Gf f1 = d(m[1][0], m[2][2], m[2][0], m[1][2]);
+    const Gf f2 = d(m[1][0], m[2][1], m[2][0], m[1][1]);
+    const Gf det = add(sub(mul(m[0][0], f0), mul(m[0][1], f1)), mul(m[0][2], f2));
+    Gf inv[3][3];  // inv[col][row]
+    inv[0][0] = div(f0, det);
+    inv[1][0] = div(neg(f1), det);
+    inv[2][0] = div(f2, det);
+    inv[0][1] = div(neg(d(m[0][1], m[2][2], m[2][1], m[0][2])), det);
+    inv[1][1] = div(d(m[0][0], m[2][2], m[2][0], m[0][2]), det);
+    inv[2][1] = div(neg(d(m[0][0], m[2][1], m[2][0], m[0][1])), det);
+    inv[0][2] = div(d(m[0][1], m[1][2], m[1][1], m[0][2]), det);
+    inv[1][2] = div(neg(d(m[0][0], m[1][2], m[1][0], m[0][2])), det);
+    inv[2][2] = div(d(m[0][0], m[1][1], m[1][0], m[0][1]), det);
+    for (int c = 0; c < 3; ++c)
+        for (int w = 0; w < 3; ++w) r[c][w] = inv[w][c];  // transpose
+}
+
+// rotation_matrix_{x,y,z} (:444-486) of a run-time angle in degrees
+Gm rot_deg(int axis, float deg) {
+    const float a = mul(cst(kDegToRad), run(deg)).v;
+    return rot(axis, run(gl_cos(a)), run(gl_sin(a)));
+}
+
 }  // namespace
 
 float gl_sin(float a) { return gallivm_sincos(a, false); }
@@ -268,6 +298,32 @@ void reference_view_gl(float time, float unproj[16], float view[16]) {
             if (unproj) unproj[c * 4 + w] = U.m[c][w].v;
             if (view) view[c * 4 + w] = V.m[c][w].v;
         }
+}
+
+// intersect_box_object's transforms (:650-652, :718) as llvmpipe evaluates
+// them: local_to_world = calc_transform_matrix(position, angles) (:529-532:
+// translation_matrix * (mat4(1) * Rz(yaw) * Rx(pitch) * Ry(roll))), its
+// Mesa inverse, and transpose(inverse(mat3(local_to_world))). The object's
+// fields are run-time values (objects[] is indexed by the loop counter), so
+// only the functions' own constants fold. Column-major outputs (m[col][row]
+// at col * 4 + row; the normal matrix at col * 3 + row). Probed bit-exact
+// against llvmpipe on the shipped scene (tests/golden/make_box_golden.py).
+void reference_box_transforms(const float pos[3], const float ang[3], float l2w[16], float w2l[16],
+                              float nrm[9]) {
+    Gm T = ident();
+    for (int k = 0; k < 3; ++k) T.m[3][k] = run(pos[k]);
+    const Gm R = mul(mul(mul(ident(), rot_deg(2, ang[1])), rot_deg(0, ang[0])), rot_deg(1, ang[2]));
+    const Gm L = mul(T, R);
+    const Gm W = inverse(L);
+    Gf N[3][3];
+    normal_matrix(L, N);
+    for (int c = 0; c < 4; ++c)
+        for (int w = 0; w < 4; ++w) {
+            l2w[c * 4 + w] = L.m[c][w].v;
+            w2l[c * 4 + w] = W.m[c][w].v;
+        }
+    for (int c = 0; c < 3; ++c)
+        for (int w = 0; w < 3; ++w) nrm[c * 3 + w] = N[c][w].v;
 }
 
 }  // namespace rtamd

@@ -208,6 +208,9 @@ float gl_sin(float a);  // gallivm's polynomial sin / cos (run-time GLSL sin / c
 float gl_cos(float a);
 void reference_orbit(float time, float *speed, float pos[3], float *yaw);
 void reference_view_gl(float time, float unproj[16], float view[16]);
+// a box object's local_to_world, world_to_local and normal matrix as
+// llvmpipe evaluates intersect_box_object (column-major)
+void reference_box_transforms(const float pos[3], const float ang[3], float l2w[16], float w2l[16], float nrm[9]);
 
 // rt_kernel.hip. Clears p.sched when the launch does not use the queued
 // distribution (so the caller knows whether the counter slot is in use).

@@ -193,21 +193,33 @@ int rt_reference_lights(rt_light out[RT_REFERENCE_LIGHTS]) {
     return RT_OK;
 }
 
+int rt_object_transforms(const rt_object *obj, float l2w[16], float w2l[16], float nrm[9]) {
+    if (!obj || !l2w || !w2l || !nrm) {
+        set_error("rt_object_transforms: null argument");
+        return RT_ERR_INVALID;
+    }
+    reference_box_transforms(obj->position, obj->angles, l2w, w2l, nrm);
+    return RT_OK;
+}
+
 // raytrace_compute.glsl:236-237 (scaled_time), :261-321 (objects)
 int rt_reference_objects(float time, rt_object out[RT_REFERENCE_OBJECTS]) {
     if (!out) { set_error("rt_reference_objects: null out"); return RT_ERR_INVALID; }
-    const float st = time * 0.4f;
+    // scaled_time * k = (time * time_scale) * k, which the reference's GL
+    // compiles as time * (time_scale * k) (a product by a constant times
+    // another constant folds; probed on llvmpipe)
+    auto st = [time](float k) { return time * (0.4f * k); };
     float zero[3] = {0, 0, 0};
     float mn0[3] = {-11, -11, -11}, mx0[3] = {11, 11, 11};
     make_object(out[0], mn0, mx0, -1.0f, 0, 0, 0, 0, 0, 0, RT_MAT_WALL);
     // run-time sin as the reference's GL evaluates it (rt_camera.cpp)
-    const float s = 0.5f * gl_sin(st * 0.5f) + 1.5f;
+    const float s = 0.5f * gl_sin(st(0.5f)) + 1.5f;
     float mn1[3] = {-1.0f * s, -1.0f * s, -1.0f * s}, mx1[3] = {1.0f * s, 1.0f * s, 1.0f * s};
-    make_object(out[1], mn1, mx1, -1.0f, 0, 0, gl_sin(st * 3.0f), 0, st * 90.0f, 0, RT_MAT_MIRROR);
+    make_object(out[1], mn1, mx1, -1.0f, 0, 0, gl_sin(st(3.0f)), 0, st(90.0f), 0, RT_MAT_MIRROR);
     float mn2[3] = {-10, -10, -1}, mx2[3] = {10, 10, 1};
-    make_object(out[2], mn2, mx2, -1.0f, 0, 0, -3, gl_sin(st * 5.0f) * 10.0f, 45.0f, 0, RT_MAT_GREEN_GLASS);
+    make_object(out[2], mn2, mx2, -1.0f, 0, 0, -3, gl_sin(st(5.0f)) * 10.0f, 45.0f, 0, RT_MAT_GREEN_GLASS);
     float mn3[3] = {-1, -1, -2}, mx3[3] = {1, 1, 2};
-    make_object(out[3], mn3, mx3, -1.0f, 3, 4, 1, 45.0f + st * 45.0f, 0, 45.0f + st * 180.0f, RT_MAT_BLUE_GLASS);
+    make_object(out[3], mn3, mx3, -1.0f, 3, 4, 1, 45.0f + st(45.0f), 0, 45.0f + st(180.0f), RT_MAT_BLUE_GLASS);
     make_object(out[4], zero, zero, 2.0f, -3, 4, 1, 0, 0, 0, RT_MAT_RED_GLASS);
     return RT_OK;
 }
@@ -750,18 +762,18 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             // is a sphere of radius |r|: the test only sees r*r, :588)
             smeta.push_back({i, o.material, std::fabs(o.radius), 0});
         } else {
-            const M4 L = transform(o.position, o.angles);
-            const M4 W = inverse(L);
+            // the transforms as the reference's GL evaluates them per ray (rt_camera.cpp)
+            float L[16], W[16], N[9];
+            reference_box_transforms(o.position, o.angles, L, W, N);
             BoxRec b{};
             for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) {
-                    b.w2l[r * 4 + c] = static_cast<float>(W.m[c][r]);
-                    b.l2w[r * 4 + c] = static_cast<float>(L.m[c][r]);
+                for (int c = 0; c < 4; ++c) {  // stored row-major
+                    b.w2l[r * 4 + c] = W[c * 4 + r];
+                    b.l2w[r * 4 + c] = L[c * 4 + r];
                 }
-            // transpose(inverse(mat3(L))) = transpose of inverse(L)'s 3x3 block;
-            // stored row-major: nrm[r][c] = inverse(L)[c][r] read transposed.
+            // the normal matrix transpose(inverse(mat3(L))), stored row-major
             for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) b.nrm[r * 3 + c] = static_cast<float>(W.m[r][c]);
+                for (int c = 0; c < 3; ++c) b.nrm[r * 3 + c] = N[c * 3 + r];
             std::memcpy(b.mins, o.box_mins, 12);
             std::memcpy(b.maxs, o.box_maxs, 12);
             b.obj_index = i;
@@ -773,12 +785,13 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             // Lights strictly inside the box by a margin (float64): a shadow
             // segment that starts inside the box then ends inside it too (its
             // end is the light + 0.01 n, :808-809), so the box cannot occlude.
+            const M4 Wd = inverse(transform(o.position, o.angles));  // culling only (float64)
             for (int j = 0; j < n_lights && j < 32; ++j) {
                 double lp[3];
                 bool in = true;
                 for (int r = 0; r < 3; ++r) {
-                    lp[r] = W.m[0][r] * lights[j].position[0] + W.m[1][r] * lights[j].position[1] +
-                            W.m[2][r] * lights[j].position[2] + W.m[3][r];
+                    lp[r] = Wd.m[0][r] * lights[j].position[0] + Wd.m[1][r] * lights[j].position[1] +
+                            Wd.m[2][r] * lights[j].position[2] + Wd.m[3][r];
                     const double m = 0.05 + 1e-4 * (std::fabs(o.box_mins[r]) + std::fabs(o.box_maxs[r]) +
                                                     std::fabs(lp[r]));
                     in = in && std::isfinite(lp[r]) && o.box_mins[r] + m < lp[r] && lp[r] < o.box_maxs[r] - m;

@@ -26,7 +26,10 @@
  *   P4 (probe)    :401  the colour is replaced by an intermediate value
  *                 (ray dir, closest hit, shadow mask, normal, hit point,
  *                 and (probe 5) the camera matrices: pixel (x,y) holds element
- *                 [x%4][y%4] of inverse(proj*view), view and proj).
+ *                 [x%4][y%4] of inverse(proj*view), view and proj; (probe 7)
+ *                 object (x/4)'s box transforms: element [x%4][y%4] of
+ *                 calc_transform_matrix, its inverse and the normal matrix
+ *                 transpose(inverse(mat3(.))) as intersect_box_object forms them).
  * The output texture is RGBA32F (unclamped floats) instead of the shipped
  * RGBA8 (main.cpp:152-159,223); alpha is always 0 (raytrace_compute.glsl:404).
  */
@@ -268,13 +271,20 @@ static char *build_source(const char *objects_glsl, int max_depth, int crop, int
     }
     /* P4 */
     if (probe) {
-        snprintf(buf, sizeof buf, "const int GLREF_PROBE = %d;\nvec3 glref_probe(Ray r);\nvoid main()", probe);
+        snprintf(buf, sizeof buf,
+                 "const int GLREF_PROBE = %d;\nvec3 glref_probe(Ray r);\n"
+                 "mat4 calc_transform_matrix(vec3 position, vec3 angles);\nvoid main()", probe);
         if (patch(&s, "P4a", "void main()", buf)) goto fail;
         if (patch(&s, "P4b", "vec3 final_color = recursive_raytrace(world_ray, MAX_RAYTRACE_DEPTH);",
                   "vec3 final_color = glref_probe(world_ray);\n"
                   "\tif (GLREF_PROBE == 5) final_color = vec3(inverse_proj_mat[pixel.x % 4][pixel.y % 4],"
                   " view_mat[pixel.x % 4][pixel.y % 4], proj_mat[pixel.x % 4][pixel.y % 4]);\n"
-                  "\tif (GLREF_PROBE == 6) final_color = vec3((proj_mat * view_mat)[pixel.x % 4][pixel.y % 4], 0.0, 0.0);")) goto fail;
+                  "\tif (GLREF_PROBE == 6) final_color = vec3((proj_mat * view_mat)[pixel.x % 4][pixel.y % 4], 0.0, 0.0);\n"
+                  "\tif (GLREF_PROBE == 7) { int k = (pixel.x / 4) % objects_count;"
+                  " mat4 lw = calc_transform_matrix(objects[k].position, objects[k].angles);"
+                  " mat4 wl = inverse(lw); mat3 nm = transpose(inverse(mat3(lw)));"
+                  " final_color = vec3(lw[pixel.x % 4][pixel.y % 4], wl[pixel.x % 4][pixel.y % 4],"
+                  " (pixel.x % 4 < 3 && pixel.y % 4 < 3) ? nm[pixel.x % 4][pixel.y % 4] : 0.0); }")) goto fail;
         size_t pl = strlen(PROBE_FN);
         s.s = (char *)realloc(s.s, s.n + pl + 1);
         memcpy(s.s + s.n, PROBE_FN, pl + 1);

@@ -27,6 +27,7 @@ def lib():
         L.oracle_reference_objects.argtypes = [C.c_float, C.c_void_p]
         L.oracle_reference_camera.argtypes = [C.c_float, C.c_void_p]
         L.oracle_camera_matrices.argtypes = [C.c_void_p, C.c_float, C.c_void_p]
+        L.oracle_object_transforms.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_set_f64_frame_constants.argtypes = [C.c_int]
         _lib = L
     return _lib

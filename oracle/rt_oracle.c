@@ -179,34 +179,6 @@ static m4 inverse4(m4 a) {
     return r;
 }
 
-/* transpose(inverse(mat3(L))) — the normal matrix of :718. inverse(mat3) as
- * Mesa's builtin lowers it (probed bit-exact against llvmpipe): cofactors,
- * det = (m00*c00 - m01*c10') + m02*c20', then adj / det. */
-static float d2(float a, float b, float c, float e) { return a * b - c * e; }
-static m3 normal_matrix(m4 l) {
-    float m[3][3];
-    for (int c = 0; c < 3; c++)
-        for (int r = 0; r < 3; r++) m[c][r] = l.m[c][r];
-    float f0 = d2(m[1][1], m[2][2], m[2][1], m[1][2]);
-    float f1 = d2(m[1][0], m[2][2], m[2][0], m[1][2]);
-    float f2 = d2(m[1][0], m[2][1], m[2][0], m[1][1]);
-    float det = m[0][0] * f0 - m[0][1] * f1 + m[0][2] * f2;
-    float inv[3][3];
-    inv[0][0] = f0 / det;
-    inv[1][0] = -f1 / det;
-    inv[2][0] = f2 / det;
-    inv[0][1] = -d2(m[0][1], m[2][2], m[2][1], m[0][2]) / det;
-    inv[1][1] = d2(m[0][0], m[2][2], m[2][0], m[0][2]) / det;
-    inv[2][1] = -d2(m[0][0], m[2][1], m[2][0], m[0][1]) / det;
-    inv[0][2] = d2(m[0][1], m[1][2], m[1][1], m[0][2]) / det;
-    inv[1][2] = -d2(m[0][0], m[1][2], m[1][0], m[0][2]) / det;
-    inv[2][2] = d2(m[0][0], m[1][1], m[1][0], m[0][1]) / det;
-    m3 r;
-    for (int c = 0; c < 3; c++)
-        for (int row = 0; row < 3; row++) r.m[c][row] = inv[row][c];
-    return r;
-}
-
 /* :432-437 */
 static m4 translation_matrix(v3 t) {
     m4 r = ident4();
@@ -374,21 +346,10 @@ static m4 frame_unprojection(const rt_camera *cam, float time) {
     gl_reference_matrices(time, &inv, NULL, NULL);
     return inv;
 }
-static void object_transforms(v3 pos, v3 ang, m4 *l2w, m4 *w2l, m3 *nrm) {
-    if (!g_f64_frame) {
-        *l2w = calc_transform_matrix(pos, ang);
-        *w2l = inverse4(*l2w);
-        *nrm = normal_matrix(*l2w);
-        return;
-    }
-    dm4 L = d_transform(pos, ang), Wl = d_inverse(L);
-    *l2w = d_round(L);
-    *w2l = d_round(Wl);
-    /* transpose(inverse(mat3(L))) = transpose of the upper-left 3x3 of
-     * inverse(L) (L is affine) */
-    for (int c = 0; c < 3; c++)
-        for (int r = 0; r < 3; r++) nrm->m[c][r] = (float)Wl.m[r][c];
-}
+/* per-object transforms of intersect_box_object (:650-652, :718): as
+ * llvmpipe evaluates them (gl_object_transforms below) */
+static void gl_object_transforms(v3 pos, v3 ang, m4 *l2w, m4 *w2l, m3 *nrm);
+static void object_transforms(v3 pos, v3 ang, m4 *l2w, m4 *w2l, m3 *nrm) { gl_object_transforms(pos, ang, l2w, w2l, nrm); }
 
 /* ---- reference scene ------------------------------------------------- */
 static void set_mat(rt_material *m, v4 amb, v4 dif, v4 spe, float shin, v4 emi, float refl, float transp,
@@ -603,17 +564,72 @@ static void gl_reference_matrices(float time, m4 *inv, m4 *view, m4 *proj) {
         }
 }
 
-/* :236-237, :261-321 */
+/* The box transforms of intersect_box_object as llvmpipe evaluates them:
+ * the object's fields are run-time values (objects[] is indexed by the loop
+ * counter), the functions' own constants fold (gv rules); the normal matrix
+ * transpose(inverse(mat3(L))) with Mesa's mat3 inverse (normal_matrix). */
+static gv gv_div(gv a, gv det) {
+    if (a.kind == 1 && det.kind == 1) return gv_c(a.v / det.v);
+    if (a.kind == 1 && a.v == 0.0f) return gv_c(0.0f);
+    return gv_r(a.v / det.v);
+}
+static gm gm_rot_deg(int axis, float deg) { /* rotation_matrix_{x,y,z} of a run-time angle */
+    float a = gv_mul(gv_c(DEG_TO_RAD), gv_r(deg)).v;
+    return gm_rot(axis, gv_r(gv_sincos(a, 1)), gv_r(gv_sincos(a, 0)));
+}
+static void gl_object_transforms(v3 pos, v3 ang, m4 *l2w, m4 *w2l, m3 *nrm) {
+    gm T = gm_ident();
+    T.m[3][0] = gv_r(pos.x); T.m[3][1] = gv_r(pos.y); T.m[3][2] = gv_r(pos.z);
+    gm R = gm_mul(gm_mul(gm_mul(gm_ident(), gm_rot_deg(2, ang.y)), gm_rot_deg(0, ang.x)), gm_rot_deg(1, ang.z));
+    gm L = gm_mul(T, R), W = gm_inverse(L);
+    gv(*m)[4] = L.m;
+    gv f0 = gv_d(m[1][1], m[2][2], m[2][1], m[1][2]);
+    gv f1 = gv_d(m[1][0], m[2][2], m[2][0], m[1][2]);
+    gv f2 = gv_d(m[1][0], m[2][1], m[2][0], m[1][1]);
+    gv det = gv_add(gv_sub(gv_mul(m[0][0], f0), gv_mul(m[0][1], f1)), gv_mul(m[0][2], f2));
+    gv inv[3][3]; /* [col][row] */
+    inv[0][0] = gv_div(f0, det);
+    inv[1][0] = gv_div(gv_neg(f1), det);
+    inv[2][0] = gv_div(f2, det);
+    inv[0][1] = gv_div(gv_neg(gv_d(m[0][1], m[2][2], m[2][1], m[0][2])), det);
+    inv[1][1] = gv_div(gv_d(m[0][0], m[2][2], m[2][0], m[0][2]), det);
+    inv[2][1] = gv_div(gv_neg(gv_d(m[0][0], m[2][1], m[2][0], m[0][1])), det);
+    inv[0][2] = gv_div(gv_d(m[0][1], m[1][2], m[1][1], m[0][2]), det);
+    inv[1][2] = gv_div(gv_neg(gv_d(m[0][0], m[1][2], m[1][0], m[0][2])), det);
+    inv[2][2] = gv_div(gv_d(m[0][0], m[1][1], m[1][0], m[0][1]), det);
+    for (int c = 0; c < 4; c++)
+        for (int w = 0; w < 4; w++) {
+            l2w->m[c][w] = L.m[c][w].v;
+            w2l->m[c][w] = W.m[c][w].v;
+        }
+    for (int c = 0; c < 3; c++)
+        for (int w = 0; w < 3; w++) nrm->m[c][w] = inv[w][c].v; /* transpose */
+}
+
+/* Test export: gl_object_transforms of an object, column-major:
+ * out[0..16) local_to_world, out[16..32) world_to_local, out[32..41) normal. */
+void oracle_object_transforms(const rt_object *o, float out[41]) {
+    m4 l, w;
+    m3 n;
+    gl_object_transforms(ld3(o->position), ld3(o->angles), &l, &w, &n);
+    memcpy(out, l.m, 64);
+    memcpy(out + 16, w.m, 64);
+    memcpy(out + 32, n.m, 36);
+}
+
+/* :236-237, :261-321. scaled_time * k = (time * time_scale) * k is compiled
+ * as time * (time_scale * k) (constant products fold; probed on llvmpipe). */
+static float st_k(float time, float k) { return time * (0.4f * k); }
 void oracle_reference_objects(float time, rt_object out[5]) {
-    float st = time * 0.4f; /* scaled_time = time * time_scale */
     v3 z = V3(0, 0, 0);
     set_obj(&out[0], V3(-11, -11, -11), V3(11, 11, 11), -1.0f, z, z, 6);
-    float s = 0.5f * gv_sincos(st * 0.5f, 0) + 1.5f; /* run-time sin: gallivm */
-    set_obj(&out[1], mul3s(V3(-1, -1, -1), s), mul3s(V3(1, 1, 1), s), -1.0f, V3(0, 0, gv_sincos(st * 3.0f, 0)),
-            V3(0, st * 90.0f, 0), 5);
-    set_obj(&out[2], V3(-10, -10, -1), V3(10, 10, 1), -1.0f, V3(0, 0, -3), V3(gv_sincos(st * 5.0f, 0) * 10.0f, 45, 0), 3);
+    float s = 0.5f * gv_sincos(st_k(time, 0.5f), 0) + 1.5f; /* run-time sin: gallivm */
+    set_obj(&out[1], mul3s(V3(-1, -1, -1), s), mul3s(V3(1, 1, 1), s), -1.0f, V3(0, 0, gv_sincos(st_k(time, 3.0f), 0)),
+            V3(0, st_k(time, 90.0f), 0), 5);
+    set_obj(&out[2], V3(-10, -10, -1), V3(10, 10, 1), -1.0f, V3(0, 0, -3),
+            V3(gv_sincos(st_k(time, 5.0f), 0) * 10.0f, 45, 0), 3);
     set_obj(&out[3], V3(-1, -1, -2), V3(1, 1, 2), -1.0f, V3(3, 4, 1),
-            V3(45.0f + st * 45.0f, 0, 45.0f + st * 180.0f), 4);
+            V3(45.0f + st_k(time, 45.0f), 0, 45.0f + st_k(time, 180.0f)), 4);
     set_obj(&out[4], z, z, 2.0f, V3(-3, 4, 1), z, 2);
 }
 

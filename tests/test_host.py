@@ -248,6 +248,30 @@ def test_reference_camera_matches_llvmpipe_golden_vectors():
         assert np.array_equal(np.array(cam.position[:], np.float32), o)
 
 
+def test_box_transforms_match_llvmpipe_golden_vectors():
+    """rt_object_transforms — the matrices the scene builder stores for every
+    box — equals llvmpipe's calc_transform_matrix, inverse and normal matrix
+    of intersect_box_object (:650-652, :718) bit for bit for the shipped
+    scene's four boxes at 32 times (tests/golden/box_llvmpipe.npz, from the
+    reference's own functions: tests/golden/make_box_golden.py); the object
+    tables (rt_reference_objects) follow llvmpipe's scaled_time folding.
+    Rows 0-2 — every entry the shader consumes ((M * v).xyz, mat3(M)) and the
+    scene builder stores — are compared bit for bit; row 3 by value (llvmpipe
+    leaves -0.0 in two of its dead entries)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "box_llvmpipe.npz"))
+    L, W, N = (np.zeros(n, np.float32) for n in (16, 16, 9))
+    used = np.array([r < 3 for c in range(4) for r in range(4)])
+    for i, t in enumerate(z["time"]):
+        objs = rt.reference_objects(float(t))
+        for k in range(4):  # the boxes (object 4 is the sphere)
+            assert rt.lib().rt_object_transforms(C.byref(objs[k]), L.ctypes.data, W.ctypes.data, N.ctypes.data) == 0
+            for name, mine in (("l2w", L), ("w2l", W), ("nrm", N)):
+                ref = z[name][i, k]
+                bitwise = used if name != "nrm" else np.ones(9, bool)
+                assert np.array_equal(mine[bitwise].view(np.uint32), ref[bitwise].view(np.uint32)), (float(t), k, name)
+                assert np.array_equal(mine, ref), (float(t), k, name)
+
+
 @pytest.mark.timeout(600)
 def test_host_code_under_address_and_ub_sanitizers():
     """make asan: the host C++ — scene description parser,
