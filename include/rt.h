@@ -299,7 +299,9 @@ int rt_context_set(rt_context *ctx, int option, int value);
 int rt_last_kernel_ms(rt_context *ctx, float *ms);
 
 /* RGBA8 unorm packing of a float frame as the shipped GL_RGBA8 surface stores
- * it (clamp to [0,1], round to nearest). Host memory, n pixels. */
+ * it (NaN -> 0, clamp to [0,1], v * 255 rounded to nearest even, as the
+ * reference's GL converts; pinned by tests/golden/rgba8_llvmpipe.npz). Host
+ * memory, n pixels. */
 int rt_pack_rgba8(const float *rgba32f, size_t n_pixels, uint8_t *out_rgba8);
 
 /* Headless image dump (replaces the display pass, draw_screen_*.glsl and

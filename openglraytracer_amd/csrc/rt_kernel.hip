@@ -1254,9 +1254,11 @@ __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     return (blk * p.n_shards + p.shard) * p.block_rows + (local - blk * p.block_rows);
 }
 
+// GL_RGBA8 unorm conversion as the reference's GL applies it: NaN -> 0,
+// clamp, v * 255 rounded to nearest even (rt_pack_rgba8)
 __device__ __forceinline__ uint32_t unorm8(float v) {
     v = v != v ? 0.0f : gmin(gmax(v, 0.0f), 1.0f);
-    return static_cast<uint32_t>(v * 255.0f + 0.5f);
+    return static_cast<uint32_t>(__builtin_rintf(v * 255.0f));
 }
 
 // One pixel's colour into the launch's surface (float4 or GL_RGBA8 bytes).

@@ -34,6 +34,8 @@ def lib():
         L.glref_shader_hash.restype = C.c_ulonglong
         L.glref_shader_size.restype = C.c_long
         L.glref_init.restype = C.c_int
+        L.glref_render_rgba8.argtypes = [C.c_char_p, C.c_int, C.c_float] + [C.c_int] * 6 + [C.c_void_p]
+        L.glref_render_rgba8.restype = C.c_int
         _lib = L
     return _lib
 
@@ -79,3 +81,14 @@ def render(objects, width, height, max_depth=0, time=0.0, crop=None, probe=0, re
     if rc != 0:
         raise RuntimeError("glref: " + lib().glref_last_error().decode())
     return out, times[:repeats]
+
+
+def render_rgba8(objects, width, height, max_depth=0, time=0.0, crop=None):
+    """The same render into the shipped app's GL_RGBA8 surface: uint8 (h, w, 4)."""
+    x0, y0, w, h = crop if crop is not None else (0, 0, width, height)
+    out = np.zeros((h, w, 4), np.uint8)
+    src = objects_glsl(objects).encode() if objects is not None else None
+    rc = lib().glref_render_rgba8(src, max_depth, C.c_float(time), width, height, x0, y0, w, h, out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("glref: " + lib().glref_last_error().decode())
+    return out

@@ -323,7 +323,10 @@ static int cmp_d(const void *a, const void *b) {
  * Returns 0 or -1 (glref_last_error()).
  */
 static int run_program(char *src, float time_s, int width, int height, int crop, int x0, int y0, int w,
-                       int h, int repeats, float *out, double *times);
+                       int h, int repeats, void *out, double *times);
+/* output surface: 0 RGBA32F (default), 1 the shipped app's GL_RGBA8
+ * (main.cpp:152-159, :223) read back as bytes */
+static int g_rgba8 = 0;
 
 int glref_render(const char *objects_glsl, int max_depth, float time_s, int width, int height,
                  int x0, int y0, int w, int h, int probe, int repeats, float *out, double *times) {
@@ -338,6 +341,18 @@ int glref_render(const char *objects_glsl, int max_depth, float time_s, int widt
     return run_program(src, time_s, width, height, crop, x0, y0, w, h, repeats, out, times);
 }
 
+/* The same render into the shipped app's GL_RGBA8 image (glBindImageTexture
+ * GL_RGBA8, main.cpp:223): out receives w*h*4 bytes, the driver's float ->
+ * unorm8 conversion of imageStore(vec4(final_color, 0.0)) (:404). */
+int glref_render_rgba8(const char *objects_glsl, int max_depth, float time_s, int width, int height, int x0, int y0,
+                       int w, int h, unsigned char *out) {
+    g_rgba8 = 1;
+    int rc = glref_render(objects_glsl, max_depth, time_s, width, height, x0, y0, w, h, 0, 0, (float *)(void *)out,
+                          NULL);
+    g_rgba8 = 0;
+    return rc;
+}
+
 /* Arithmetic probe: run an arbitrary compute shader (NOT the reference) that
  * writes rgba32f image unit 0 of size w x h, to study llvmpipe's builtins
  * (sin/cos/pow/inverse/normalize) that the reference's results depend on. */
@@ -350,7 +365,7 @@ int glref_run_source(const char *source, float time_s, int w, int h, float *out)
 }
 
 static int run_program(char *src, float time_s, int width, int height, int crop, int x0, int y0, int w,
-                       int h, int repeats, float *out, double *times) {
+                       int h, int repeats, void *out, double *times) {
     GLuint sh = p_glCreateShader(GL_COMPUTE_SHADER);
     const GLchar *srcs[1] = {src};
     p_glShaderSource(sh, 1, srcs, NULL);
@@ -380,9 +395,9 @@ static int run_program(char *src, float time_s, int width, int height, int crop,
     GLuint tex;
     p_glGenTextures(1, &tex);
     p_glBindTexture(GL_TEXTURE_2D, tex);
-    p_glTexStorage2D(GL_TEXTURE_2D, 1, GL_RGBA32F, w, h);
+    p_glTexStorage2D(GL_TEXTURE_2D, 1, g_rgba8 ? GL_RGBA8 : GL_RGBA32F, w, h);
     p_glUseProgram(prog);
-    p_glBindImageTexture(0, tex, 0, GL_FALSE, 0, GL_WRITE_ONLY, GL_RGBA32F);
+    p_glBindImageTexture(0, tex, 0, GL_FALSE, 0, GL_WRITE_ONLY, g_rgba8 ? GL_RGBA8 : GL_RGBA32F);
     p_glUniform1f(p_glGetUniformLocation(prog, "time"), time_s);
     if (crop) {
         p_glUniform2i(p_glGetUniformLocation(prog, "glref_size"), width, height);
@@ -397,7 +412,7 @@ static int run_program(char *src, float time_s, int width, int height, int crop,
         if (it >= 0 && times) times[it] = t1 - t0;
     }
     p_glMemoryBarrier(GL_TEXTURE_UPDATE_BARRIER_BIT);
-    p_glGetTexImage(GL_TEXTURE_2D, 0, GL_RGBA, GL_FLOAT, out);
+    p_glGetTexImage(GL_TEXTURE_2D, 0, GL_RGBA, g_rgba8 ? GL_UNSIGNED_BYTE : GL_FLOAT, out);
     GLenum e = p_glGetError();
     if (e != GL_NO_ERROR) { set_err("GL error 0x%x", e); rc = -1; }
     p_glDeleteTextures(1, &tex);

@@ -439,6 +439,34 @@ def test_scene_update_animation(gpu_ctx):
     sc.close()
 
 
+def test_rgba8_surface_matches_the_gl_rgba8_render(gpu_ctx):
+    """rt_render(cam = NULL) into the RGBA8 surface (RT_OUTPUT_RGBA8) — the
+    shipped app's GL_RGBA8 texture, main.cpp:152-159, :223 — equals, byte for
+    byte, the reference's own render stored by its GL into that format
+    (tests/golden/rgba8_llvmpipe.npz: GL rounds exact halves to even)."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rgba8_llvmpipe.npz"))
+    names = sorted(k[:-len("_rgba8")] for k in z.files if k.endswith("_rgba8"))
+    gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA8)
+    try:
+        for n in names:
+            w, h, depth, t, x0, y0, cw, ch = z[n + "_meta"]
+            w, h, depth, x0, y0, cw, ch = (int(v) for v in (w, h, depth, x0, y0, cw, ch))
+            scene = str(z[n + "_scene"])
+            objs = rt.reference_objects(float(t)) if scene == "shipped" else scenes.CONFIGS[scene][0]()
+            sc = rt.Scene(gpu_ctx, objs)
+            try:
+                out = np.zeros((ch, w, 4), np.uint8)
+                rc = rt.lib().rt_render(gpu_ctx.handle, sc.handle, None, float(t), w, h, depth, y0, y0 + ch,
+                                        out.ctypes.data, 0, None)
+                assert rc == 0, rt.lib().rt_last_error()
+            finally:
+                sc.close()
+            assert np.array_equal(out[:, x0:x0 + cw], z[n + "_rgba8"]), n
+    finally:
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA32F)
+
+
 @pytest.mark.parametrize("cfg,w,h", [("shipped", 160, 90), ("config3", 256, 144)])
 def test_rgba8_surface_equals_packed_float_frame(gpu_ctx, cfg, w, h):
     """RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 texture, main.cpp:152-159): the

@@ -110,6 +110,23 @@ def test_pack_rgba8_matches_gl_unorm():
     assert out[1].tolist() == [0, 128, 0, 255]
 
 
+def test_pack_rgba8_matches_the_gl_rgba8_surface():
+    """rt_pack_rgba8 of the reference's float render equals, byte for byte,
+    the same render stored by the reference's GL into the shipped app's
+    GL_RGBA8 surface (main.cpp:152-159, :223; tests/golden/rgba8_llvmpipe.npz,
+    tests/golden/make_rgba8_golden.py) — including the exact halves, which GL
+    rounds to even."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "rgba8_llvmpipe.npz"))
+    names = sorted(k[:-len("_rgba8")] for k in z.files if k.endswith("_rgba8"))
+    halves = 0
+    for n in names:
+        f = z[n + "_rgba32f"]
+        assert np.array_equal(rt.pack_rgba8(f), z[n + "_rgba8"]), n
+        v = np.clip(f, 0, 1) * np.float32(255)
+        halves += int((v - np.floor(v) == 0.5).sum())
+    assert halves > 0  # the fixtures hold exact halves (round-to-even pinned)
+
+
 def test_errors_without_gpu_are_reported_not_raised_natively():
     lib = rt.lib()
     h = C.c_void_p()
