@@ -558,7 +558,9 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         // spill at the 80-VGPR cap): reading both successors' records before
         // the node test (config 4 22.0 -> 24.7 ms, config 3 1.058 -> 1.128 ms);
         // loading the wide-mask words in phong ahead of the shading math
-        // (22.0 -> 23.6 ms, 1.058 -> 1.149 ms).
+        // (22.0 -> 23.6 ms, 1.058 -> 1.149 ms); a speculative second leaf per
+        // lane while other lanes look for their first (config 4 18.0 -> 19.0
+        // ms, config 3 1.018 -> 1.060 ms).
         int held = 0;  // (count << 24) | first sphere of the held leaf
 #ifndef RT_BVH_FIXED
         // the ray's octant picks its traversal order (nearer child first)
