@@ -385,11 +385,18 @@ __device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, 
 __device__ __forceinline__ float root_floor(float qa2) {
     return (qa2 >= 0x1p-100f && qa2 <= 0x1p100f) ? qa2 * 0x1p-100f : __builtin_nanf("");
 }
+// sqrt(qd) of the sphere tests, correctly rounded: the short form when every
+// active lane's operand is in its range (qd >= 2^-96; +inf included), else
+// the IEEE sequence (config 4 18.20 -> 17.94 ms, config 3 1.030 -> 1.001 ms)
+__device__ __forceinline__ float sphere_sqrt(float qd) {
+    if (__all(qd >= 0x1p-96f)) return sqrt_short(qd);
+    return sqrtf(qd);
+}
 // intersect_sphere_object's t (:586-625) from the ray-invariant terms.
 __device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float qa4, float floor, bool &inside) {
     const float qd = qb * qb - qa4 * qc;
     if (qd < 0.0f) return -1.0f;
-    const float sq = sqrtf(qd);
+    const float sq = sphere_sqrt(qd);
     const float n1 = -qb + sq, n2 = -qb - sq;
 #ifndef RT_TWO_DIV
     if (fminf(fabsf(n1), fabsf(n2)) >= floor) {
@@ -411,7 +418,7 @@ __device__ __forceinline__ bool sphere_blocks(float qb, float qc, float qa2, flo
     const float qd = qb * qb - qa4 * qc;
     if (!(qd >= 0.0f)) return false;
 #ifndef RT_TWO_DIV
-    const float sq = sqrtf(qd);
+    const float sq = sphere_sqrt(qd);
     const float n1 = -qb + sq, n2 = -qb - sq;
     if (fminf(fabsf(n1), fabsf(n2)) >= floor) {
         if (n1 < 0.0f) return false;
@@ -746,6 +753,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         } else {  // 32-bit masks: half the bit arithmetic
             uint32_t cand = need && !hit ? static_cast<uint32_t>(mask) : 0u;
             while (__any(cand != 0u)) {
+                RT_STAT(12, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (cand) {
                     exact(__builtin_ctz(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
