@@ -76,11 +76,17 @@ __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + (a.y * b.y
 // to a scale-up of tiny x, v_sqrt, two one-ulp probes with fma, the
 // scale-down and a class fix-up. For operands of moderate magnitude the scale
 // steps are identities and the fix-ups return their input, so the arithmetic
-// that remains — written out below in the same order — is the same correctly
-// rounded result in fewer instructions, and a reciprocal shared by several
-// quotients is refined once. Valid ranges: div_r needs b normal with
-// |b| in [2^-60, 2^60] and a = +0 or |a| in [2^-60, 2^60]; sqrt_short needs
-// x >= 2^-96 (or +inf). Callers prove the range or check it per wave.
+// that remains is the same correctly rounded result in fewer instructions:
+//  * the refined reciprocal r = rcp + one fma step IS the correctly rounded
+//    1 / b (on gfx950, for every significand: tools/probes/arith_probe.hip,
+//    exhaustive over three binade pairs, profiles/r02k_arith_probe.log);
+//  * so one correction of q = a r gives the correctly rounded quotient
+//    (Markstein: r correctly rounded and q faithful => q + (a - b q) r,
+//    rounded once, is RN(a / b); also 3.2e9 random pairs, 0 mismatches);
+//  * a reciprocal shared by several quotients is refined once.
+// Valid ranges: div_r needs b normal with |b| in [2^-60, 2^60] and a = +0 or
+// |a| in [2^-60, 2^60]; sqrt_short needs x >= 2^-96 (or +inf). Callers prove
+// the range or check it per wave.
 struct Rcp {
     float b, r;
 };
@@ -91,11 +97,15 @@ __device__ __forceinline__ Rcp rcp_refined(float b) {
     return {b, r};
 }
 __device__ __forceinline__ float div_r(float a, Rcp d) {
-    float q = a * d.r;
+    const float q = a * d.r;
+#ifdef RT_DIV_TWO  // (the two-correction sequence hipcc's expansion ends with)
     float t = __builtin_fmaf(-d.b, q, a);
-    q = __builtin_fmaf(t, d.r, q);
-    t = __builtin_fmaf(-d.b, q, a);
-    return __builtin_fmaf(t, d.r, q);
+    const float q1 = __builtin_fmaf(t, d.r, q);
+    t = __builtin_fmaf(-d.b, q1, a);
+    return __builtin_fmaf(t, d.r, q1);
+#else
+    return __builtin_fmaf(__builtin_fmaf(-d.b, q, a), d.r, q);
+#endif
 }
 __device__ __forceinline__ float sqrt_short(float x) {
     const float s = __builtin_amdgcn_sqrtf(x);
@@ -103,13 +113,39 @@ __device__ __forceinline__ float sqrt_short(float x) {
     const float r = __builtin_fmaf(-dn, s, x) <= 0.0f ? dn : s;
     return __builtin_fmaf(-up, s, x) > 0.0f ? up : r;
 }
-// 1 / sqrt(d), both correctly rounded (GLSL inversesqrt as llvmpipe evaluates it)
+// 1 / sqrt(d), both correctly rounded (GLSL inversesqrt as llvmpipe evaluates
+// it): the refined reciprocal of the short square root
 __device__ __forceinline__ float inv_sqrt(float d) {
+#ifdef RT_DIV_TWO
     if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return div_r(1.0f, rcp_refined(sqrt_short(d)));
+#else
+    if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return rcp_refined(sqrt_short(d)).r;
+#endif
     return 1.0f / sqrtf(d);
 }
 // normalize(v) = v * inversesqrt(dot(v, v))
 __device__ __forceinline__ v3 normalize(v3 a) { return muls(a, inv_sqrt(dot(a, a))); }
+// inversesqrt of d = 1 + k ulp(1) (|k| <= 2048 float steps of d's bit pattern):
+// fl(1 / fl(sqrt(d))) in closed form. Above 1, fl(sqrt(1 + k 2^-23)) =
+// 1 + floor(k/2) 2^-23 and its reciprocal rounds to 1 - floor(k/2) 2^-23;
+// below 1, d = 1 - m 2^-24 gives 1 - ceil(m/2) 2^-24 and then
+// 1 + ceil(m/4) 2^-23 (the neglected higher-order terms stay far below the
+// rounding boundaries: exhaustively equal to the IEEE pair for k in
+// [-8190, 2897], tests/test_host.py::test_inv_sqrt_near_one).
+__device__ __forceinline__ bool near_one(float d) { return __float_as_uint(d) - 0x3f7ff800u <= 0x1000u; }
+__device__ __forceinline__ float inv_sqrt_near_one(float d) {
+    const int k = static_cast<int>(__float_as_uint(d)) - 0x3f800000;
+    return __uint_as_float(k >= 0 ? 0x3f800000u - static_cast<uint32_t>(k & ~1)
+                                  : 0x3f800000u + static_cast<uint32_t>((3 - k) >> 2));
+}
+// normalize() of a vector that is a unit vector up to rounding (a reflected
+// or negated unit vector): the closed form when every lane's squared length
+// is within 2048 ulps of 1, else the general path; bit-identical either way
+__device__ __forceinline__ v3 normalize_unit(v3 a) {
+    const float d = dot(a, a);
+    if (__all(near_one(d))) return muls(a, inv_sqrt_near_one(d));
+    return muls(a, inv_sqrt(d));
+}
 __device__ __forceinline__ float gmin(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float gmax(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float comp(v3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
@@ -939,7 +975,7 @@ __device__ unsigned long long rt_phase_buf[kPhaseWaves * 16];
 __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collision &c, bool valid) {
     const MatRec &m = S.mat[c.material];
     float4 dif = make_float4(0.0f, 0.0f, 0.0f, 0.0f), spe = dif;
-    const v3 view = normalize(muls(r.dir, -1.0f));
+    const v3 view = normalize_unit(muls(r.dir, -1.0f));  // ray directions are unit vectors up to rounding
     int slot = -1;  // index among the live lights (direction masks)
     for (int j = 0; j < S.nl; ++j) {
         const LightRec L = cload(S.clight + j);
@@ -956,7 +992,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
             smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
                                    S.dmask_bytes, muls(sdir, -1.0f), S.ns);
         const v3 ldir = normalize(sdir);
-        const v3 lref = normalize(reflect(muls(ldir, -1.0f), c.n));
+        const v3 lref = normalize_unit(reflect(muls(ldir, -1.0f), c.n));
         const float cos_theta = dot(ldir, c.n);
         const float cos_phi = dot(view, lref);
         const LightMatRec &q = S.lm[c.material * S.nl + j];
@@ -1434,6 +1470,9 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
         ws[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 0.5f + M[12 + k] * 1.0f;
         we[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 1.0f + M[12 + k] * 1.0f;
     }
+    // (the six perspective divisions as two shared refined reciprocals and
+    // one-correction quotients behind a per-wave range check measured slower
+    // again with the cheaper quotient: config 2 38.9 -> 40.3 us per frame)
     const v3 s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
     const v3 e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
     Ray ray;

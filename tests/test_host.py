@@ -301,3 +301,21 @@ def test_host_code_under_address_and_ub_sanitizers():
                        capture_output=True, text=True, timeout=580)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "clean" in r.stdout
+
+
+def test_inv_sqrt_near_one():
+    """The kernel's closed form of inversesqrt for squared lengths within
+    2048 float steps of 1 (rt_kernel.hip inv_sqrt_near_one, used by
+    normalize_unit) equals the two correctly rounded IEEE steps
+    fl(1 / fl(sqrt(d))) on every such d, and beyond: the whole range it is
+    exact on is [-8190, 2897] steps."""
+    k = np.arange(-8190, 2898, dtype=np.int64)
+    d = (0x3F800000 + k).astype(np.uint32).view(np.float32)
+    want = (np.float32(1.0) / np.sqrt(d)).view(np.uint32)
+    got = np.where(k >= 0, 0x3F800000 - (k & ~1), 0x3F800000 + ((3 - k) >> 2)).astype(np.uint32)
+    assert np.array_equal(got, want)
+    for edge in (-8191, 2898):  # the form's exact range ends here
+        dd = np.array([0x3F800000 + edge], np.uint32).view(np.float32)
+        w = (np.float32(1.0) / np.sqrt(dd)).view(np.uint32)[0]
+        g = 0x3F800000 - (edge & ~1) if edge >= 0 else 0x3F800000 + ((3 - edge) >> 2)
+        assert g != w
