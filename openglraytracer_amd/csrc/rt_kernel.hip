@@ -354,8 +354,9 @@ __device__ __forceinline__ float exit_num(float mn, float mx, float s, float d) 
     return (__float_as_uint(d) >> 31) ? (mn - s) : (mx - s);
 }
 __device__ __forceinline__ v3 exits(const BoxRec &b, v3 rs, v3 rd) {
-    return mk(exit_num(b.mins[0], b.maxs[0], rs.x, rd.x) / rd.x, exit_num(b.mins[1], b.maxs[1], rs.y, rd.y) / rd.y,
-              exit_num(b.mins[2], b.maxs[2], rs.z, rd.z) / rd.z);
+    const float ex = exit_num(b.mins[0], b.maxs[0], rs.x, rd.x), ey = exit_num(b.mins[1], b.maxs[1], rs.y, rd.y),
+                ez = exit_num(b.mins[2], b.maxs[2], rs.z, rd.z);
+    return mk(ex / rd.x, ey / rd.y, ez / rd.z);
 }
 // Box t for the closest-hit loop (-1 on a miss), with the slab distances the
 // collision record's face test needs (bnd: t1 when entering, t2 when leaving)
@@ -422,8 +423,11 @@ __device__ __forceinline__ float root_floor(float qa2) {
     return (qa2 >= 0x1p-100f && qa2 <= 0x1p100f) ? qa2 * 0x1p-100f : __builtin_nanf("");
 }
 // (Short divisions behind the same kind of per-wave range check measured
-// slower for the box exits, config 4 +1 %, and no gain for the camera ray's
-// six perspective divisions, config 2 +1.5 % with 8 frames per launch.)
+// slower for the box exits, config 4 +1 %, and again with one-correction
+// quotients: config 2 +2.5 %, config 3 +2.6 %, config 4 +1.7 %; for this
+// division of the sphere test, configs 3-4 +2-3 %; for the camera ray's six
+// perspective divisions, config 2 +1.5 % / +3.5 %: the per-wave check and
+// its branch cost more than the instructions saved.)
 // sqrt(qd) of the sphere tests, correctly rounded: the short form when every
 // active lane's operand is in its range (qd >= 2^-96; +inf included), else
 // the IEEE sequence (config 4 18.20 -> 17.94 ms, config 3 1.030 -> 1.001 ms)
@@ -983,14 +987,6 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         ++slot;
         const v3 lpos = mk(L.pos[0], L.pos[1], L.pos[2]);
         const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
-        // its direction-mask texel, looked up ahead of the shading math so
-        // the LDS read overlaps it (p - L = -sdir)
-        uint64_t smask = 0u;  // LDS masks: the mask; wide masks: the texel
-        if (S.gmask && valid)  // wide masks win where both exist (as in occluded)
-            smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
-        else if (S.dmask && valid)
-            smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
-                                   S.dmask_bytes, muls(sdir, -1.0f), S.ns);
         const v3 ldir = normalize(sdir);
         const v3 lref = normalize_unit(reflect(muls(ldir, -1.0f), c.n));
         const float cos_theta = dot(ldir, c.n);
@@ -1022,6 +1018,16 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         continue;
 #endif
         if (__any(need)) {
+            // its direction-mask texel (p - L = -sdir), looked up only where
+            // some lane casts the shadow ray (ahead of the shading math, to
+            // overlap the LDS read, it measured slower: config 3 0.978 vs 0.960
+            // ms, config 2 39.0 vs 38.6 us per frame, config 4 +0.5 %)
+            uint64_t smask = 0u;  // LDS masks: the mask; wide masks: the texel
+            if (S.gmask && need)  // wide masks win where both exist (as in occluded)
+                smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
+            else if (S.dmask && need)
+                smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
+                                       S.dmask_bytes, muls(sdir, -1.0f), S.ns);
             const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need);
             if (need && !shadowed) {
                 dif = nd;
