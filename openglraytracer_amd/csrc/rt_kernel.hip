@@ -84,6 +84,8 @@ __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + (a.y * b.y
 //    (Markstein: r correctly rounded and q faithful => q + (a - b q) r,
 //    rounded once, is RN(a / b); also 3.2e9 random pairs, 0 mismatches);
 //  * a reciprocal shared by several quotients is refined once.
+// (v_sqrt errs both ways — 1 ulp low on 15 % of significands, 1 ulp high on
+// 982 of 2^24 — so sqrt_short keeps both one-ulp probes.)
 // Valid ranges: div_r needs b normal with |b| in [2^-60, 2^60] and a = +0 or
 // |a| in [2^-60, 2^60]; sqrt_short needs x >= 2^-96 (or +inf). Callers prove
 // the range or check it per wave.

@@ -50,6 +50,20 @@ __global__ void exhaustive(uint32_t lo, uint32_t n, unsigned long long *cnt) {
     atomicAdd(cnt + 3, (unsigned long long)c3);
     atomicAdd(cnt + 4, (unsigned long long)c4);
 }
+// direction of v_sqrt's error: counters 8 (correct = raw + 1 ulp), 9 (correct = raw - 1 ulp), 10 (other)
+__global__ void sqrt_dir(uint32_t lo, uint32_t n, unsigned long long *cnt) {
+    unsigned up = 0, dn = 0, other = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float x = __uint_as_float(lo + i);
+        const uint32_t s = __float_as_uint(sqrtf(x)), r = __float_as_uint(__builtin_amdgcn_sqrtf(x));
+        up += s == r + 1u;
+        dn += s == r - 1u;
+        other += s != r && s != r + 1u && s != r - 1u;
+    }
+    atomicAdd(cnt + 8, (unsigned long long)up);
+    atomicAdd(cnt + 9, (unsigned long long)dn);
+    atomicAdd(cnt + 10, (unsigned long long)other);
+}
 // random pairs a, b with exponents in [2^-emax, 2^emax]
 __global__ void division(uint32_t seed, uint32_t per_thread, int emax, unsigned long long *cnt) {
     unsigned c5 = 0, c6 = 0;
@@ -69,12 +83,13 @@ __global__ void division(uint32_t seed, uint32_t per_thread, int emax, unsigned 
 }
 
 int main() {
-    unsigned long long *d = nullptr, h[8];
+    unsigned long long *d = nullptr, h[12];
     if (hipMalloc(&d, sizeof h) != hipSuccess) return 1;
     struct R { const char *name; uint32_t lo, n; } ranges[] = {
         {"[1,4)", 0x3f800000u, 1u << 24},
         {"[2^-60,2^-58)", (67u << 23), 1u << 24},
         {"[2^40,2^42)", (167u << 23), 1u << 24},
+        {"[2^-96,2^-94)", (31u << 23), 1u << 24},
     };
     for (const R &rg : ranges) {
         hipMemset(d, 0, sizeof h);
@@ -82,6 +97,10 @@ int main() {
         if (hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 2;
         printf("%-14s n=%u  raw_sqrt=%llu sqrt_short=%llu raw_rcp=%llu rcp_refined=%llu invsqrt_short=%llu\n", rg.name,
                rg.n, h[0], h[1], h[2], h[3], h[4]);
+        hipMemset(d, 0, sizeof h);
+        hipLaunchKernelGGL(sqrt_dir, dim3(4096), dim3(256), 0, 0, rg.lo, rg.n, d);
+        if (hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 4;
+        printf("%-14s v_sqrt low by 1 ulp=%llu high by 1 ulp=%llu other=%llu\n", rg.name, h[8], h[9], h[10]);
     }
     for (int emax : {4, 30, 60}) {
         hipMemset(d, 0, sizeof h);
