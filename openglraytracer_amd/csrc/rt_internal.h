@@ -43,7 +43,8 @@ struct BoxRec {
     int32_t material;
     uint32_t light_inside;  // bit j: light j strictly inside the box with margin (shadow shortcut)
     int32_t translate_only;  // w2l's 3x3 block is exactly the identity (world->local = + w2l[3,7,11])
-    int32_t pad[5];
+    float w2l_w0[3];  // w2l[r][3] * 0.0f: the w column's term of (w2l * vec4(d, 0.0)) per row (+-0 or NaN)
+    int32_t pad[2];
 };  // 48 words = 192 B
 static_assert(sizeof(BoxRec) == 192, "BoxRec layout");
 

@@ -201,6 +201,22 @@ __device__ __forceinline__ float glsl_exp2(float x) {
     return ex * poly_exp2(fp);
 }
 __device__ __forceinline__ float glsl_pow(float x, float y) { return glsl_exp2(glsl_log2(x) * y); }
+// pow(x, y) for x = max(cos_phi, 0) as the shading computes it: gmax never
+// returns NaN or a negative value, and a dot product of two normalize()d
+// vectors is at most about 3 or NaN, so glsl_log2's NaN and +inf cases are
+// never reached; its zero case becomes a select
+__device__ __forceinline__ float glsl_pow_cos(float x, float y) {
+#ifdef RT_POW_FULL
+    return glsl_pow(x, y);
+#else
+    const uint32_t i = __float_as_uint(x);
+    const float e = static_cast<float>(static_cast<int>((i >> 23) & 0xffu) - 127);
+    const float mant = __uint_as_float((i & 0x007fffffu) | 0x3f800000u);
+    const float q = div_r(mant - 1.0f, rcp_refined(mant + 1.0f));
+    const float l = x == 0.0f ? -__builtin_inff() : __builtin_fmaf(q, poly_log2(q * q), e);
+    return glsl_exp2(l * y);
+#endif
+}
 
 // Hardware sqrt (about 1 ulp, no correction steps): culling arithmetic only,
 // whose margins exceed its error by orders of magnitude.
@@ -296,13 +312,19 @@ struct Scene {
 };
 
 // Hit = the closest object so far: t and reference object index (tie-break).
+// A box's hit face is decided when the box becomes the closest (from the
+// slab distances t is the minimum / maximum of, :690-721), so the three slab
+// distances are not carried through the rest of the scan (3 VGPRs less
+// live across the sphere tests and the BVH walk).
 struct Hit {
     float t;
-    int obj;      // reference index, -1 = none
-    int slot;     // sphere slot (>= 0) or ~box slot (< 0)
-    bool inside;  // t_near < 0: the ray leaves the object (:621, :693-696)
-    v3 bnd;       // box: the slab distances t is the minimum / maximum of (:690-696)
+    int obj;   // reference index, -1 = none
+    int slot;  // sphere slot (>= 0) or ~box slot (< 0)
+    int info;  // bit 0: t_near < 0, the ray leaves the object (:621, :693-696); bits 1-2: box face
 };
+// The collision record's face (:699-705): x unless t equals the y, then the
+// z slab distance.
+__device__ __forceinline__ int box_face(float t, v3 bnd) { return t == bnd.y ? 1 : (t == bnd.z ? 2 : 0); }
 
 __device__ __forceinline__ bool closer(float t, int obj, const Hit &h) {
     // get_closest_collision (:753, :763, :773): valid when t > 0 and strictly
@@ -321,6 +343,17 @@ __device__ __forceinline__ v3 xform_dir(const float *m, v3 d) {
     return mk(m[0] * d.x + m[1] * d.y + m[2] * d.z + m[3] * 0.0f,
               m[4] * d.x + m[5] * d.y + m[6] * d.z + m[7] * 0.0f,
               m[8] * d.x + m[9] * d.y + m[10] * d.z + m[11] * 0.0f);
+}
+// (w2l * vec4(d, 0.0)).xyz of a box: the w column's products with 0.0 come
+// precomputed with the record (each is the same float product, +-0 or NaN)
+__device__ __forceinline__ v3 box_dir(const BoxRec &b, v3 d) {
+#ifdef RT_XFORM_MUL0
+    return xform_dir(b.w2l, d);
+#else
+    const float *m = b.w2l;
+    return mk(m[0] * d.x + m[1] * d.y + m[2] * d.z + b.w2l_w0[0], m[4] * d.x + m[5] * d.y + m[6] * d.z + b.w2l_w0[1],
+              m[8] * d.x + m[9] * d.y + m[10] * d.z + b.w2l_w0[2]);
+#endif
 }
 __device__ __forceinline__ v3 xform_point(const float *m, v3 p) {
     return mk(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3] * 1.0f, m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7] * 1.0f,
@@ -400,7 +433,7 @@ __device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, 
     const v3 rs = xform_point(b.w2l, start);
     const bool inside = strictly_inside(b, rs);
     if (inside && (b.light_inside & light_bit)) return false;
-    const v3 rd = xform_dir(b.w2l, dir);
+    const v3 rd = box_dir(b, dir);
     if (inside && not_nan(rd)) {
         // t = t_far > 0; occluded iff some exit distance is below 1
         return quotient_below_one(exit_num(b.mins[0], b.maxs[0], rs.x, rd.x), rd.x) ||
@@ -498,7 +531,7 @@ __device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 
             h.t = t;
             h.obj = obj;
             h.slot = s;
-            h.inside = inside;
+            h.info = inside ? 1 : 0;
         }
     }
 }
@@ -555,7 +588,7 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
 __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
-    Hit h{10000.0f, -1, 0, false, mk(0.0f, 0.0f, 0.0f)};
+    Hit h{10000.0f, -1, 0, 0};
     RT_STAT(kPrimary ? 0 : 1, valid);
     RT_STAT(kPrimary ? 13 : 2, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
     for (int b = 0; b < S.nb; ++b) {
@@ -572,8 +605,8 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         }
         v3 bnd;
         bool leaving;
-        const float t = box_t(B, rs, xform_dir(B.w2l, r.dir), inside, bnd, leaving);
-        if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, leaving, bnd};
+        const float t = box_t(B, rs, box_dir(B, r.dir), inside, bnd, leaving);
+        if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, (leaving ? 1 : 0) | (box_face(t, bnd) << 1)};
     }
     const v3 d2 = muls(r.dir, 2.0f);
     const float qa = dot(r.dir, r.dir);
@@ -921,7 +954,7 @@ __device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const
         c.material = S.smeta[h.slot].y;
         c.p = add(r.start, muls(r.dir, h.t));
         c.n = normalize(sub(c.p, pos));
-        c.inside = h.inside;
+        c.inside = h.info & 1;
         if (c.inside) c.n = muls(c.n, -1.0f);  // leaving the sphere: flip (:634-637)
     } else {
         const BoxRec &B = S.box[~h.slot];
@@ -933,13 +966,9 @@ __device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const
         } else {
             rs = xform_point(B.w2l, r.start);
         }
-        const v3 rd = xform_dir(B.w2l, r.dir);
-        const float isect = h.t;
-        const v3 boundary = h.bnd;
-        c.inside = h.inside;
-        int face = 0;
-        if (isect == boundary.y) face = 1;
-        else if (isect == boundary.z) face = 2;
+        const v3 rd = box_dir(B, r.dir);
+        c.inside = h.info & 1;
+        const int face = h.info >> 1;  // box_face, decided in the scan
         v3 n = mk(face == 0 ? 1.0f : 0.0f, face == 1 ? 1.0f : 0.0f, face == 2 ? 1.0f : 0.0f);
         if (comp(rd, face) > 0.0f) n = muls(n, -1.0f);
         const float *N = B.nrm;
@@ -990,8 +1019,18 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         const v3 lpos = mk(L.pos[0], L.pos[1], L.pos[2]);
         const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
         const v3 ldir = normalize(sdir);
-        const v3 lref = normalize_unit(reflect(muls(ldir, -1.0f), c.n));
         const float cos_theta = dot(ldir, c.n);
+#ifdef RT_REFLECT_DOT
+        const v3 lref = normalize_unit(reflect(muls(ldir, -1.0f), c.n));
+#else
+        // reflect(-ldir, n) needs dot(n, -ldir), which is -cos_theta (exact
+        // negation, commuted products) except that an exactly-zero dot may
+        // differ in the sign of its zero; that only flips signs of zero
+        // components of lref, which change cos_phi at most by the sign of a
+        // zero, and max(cos_phi, 0) is +0 for both: the result is identical
+        const v3 nl = muls(ldir, -1.0f);
+        const v3 lref = normalize_unit(sub(nl, muls(c.n, 2.0f * -cos_theta)));
+#endif
         const float cos_phi = dot(view, lref);
         const LightMatRec &q = S.lm[c.material * S.nl + j];
         const float kd = gmax(cos_theta, 0.0f);
@@ -1003,7 +1042,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
 #ifdef RT_ABLATE_POW
         ks = xs;
 #else
-        if (__any(need_pow && valid)) ks = need_pow ? glsl_pow(xs, m.shininess) : 0.0f;
+        if (__any(need_pow && valid)) ks = need_pow ? glsl_pow_cos(xs, m.shininess) : 0.0f;
 #endif
         const float4 nd = make_float4(dif.x + q.ld_md[0] * kd, dif.y + q.ld_md[1] * kd, dif.z + q.ld_md[2] * kd,
                                       dif.w + q.ld_md[3] * kd);

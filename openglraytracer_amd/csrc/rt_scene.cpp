@@ -778,6 +778,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             std::memcpy(b.maxs, o.box_maxs, 12);
             b.obj_index = i;
             b.material = o.material;
+            for (int r = 0; r < 3; ++r) b.w2l_w0[r] = b.w2l[r * 4 + 3] * 0.0f;  // the kernel adds it as is
             b.translate_only = 1;
             for (int r = 0; r < 3; ++r)
                 for (int c = 0; c < 3; ++c)
