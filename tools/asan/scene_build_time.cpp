@@ -38,8 +38,14 @@ int main() {
             }
         }
         std::sort(ms.begin(), ms.end());
-        std::printf("room + %3d spheres: scene build %.3f ms (median of 7), blob %016llx\n", n, ms[3],
-                    static_cast<unsigned long long>(hash));
+        std::vector<float4> blob;
+        rtamd::DeviceScene ds;
+        rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds);
+        // LDS per work-group: the staged blob + per-sphere camera terms and footprints + per-box camera terms
+        const long lds = 16L * (ds.blob_units + 2L * n + 1);
+        std::printf("room + %3d spheres: scene build %.3f ms (median of 7), blob %016llx, LDS %ld B (masks %d B)\n", n,
+                    ms[3], static_cast<unsigned long long>(hash), lds,
+                    ds.off_dmask >= 0 ? 16 * (ds.blob_units - ds.off_dmask) : 0);
     }
     return 0;
 }
