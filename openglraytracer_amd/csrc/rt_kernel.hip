@@ -136,9 +136,18 @@ __device__ __forceinline__ v3 normalize(v3 a) { return muls(a, inv_sqrt(dot(a, a
 // [-8190, 2897], tests/test_host.py::test_inv_sqrt_near_one).
 __device__ __forceinline__ bool near_one(float d) { return __float_as_uint(d) - 0x3f7ff800u <= 0x1000u; }
 __device__ __forceinline__ float inv_sqrt_near_one(float d) {
-    const int k = static_cast<int>(__float_as_uint(d)) - 0x3f800000;
+    const uint32_t b = __float_as_uint(d);
+#ifdef RT_BRANCHY
+    const int k = static_cast<int>(b) - 0x3f800000;
     return __uint_as_float(k >= 0 ? 0x3f800000u - static_cast<uint32_t>(k & ~1)
                                   : 0x3f800000u + static_cast<uint32_t>((3 - k) >> 2));
+#else
+    // both arms computed, then one select (as a ternary the compiler made
+    // this a divergent branch)
+    const uint32_t above = 0x3f800000u - ((b - 0x3f800000u) & ~1u);  // k >= 0
+    const uint32_t below = 0x3f800000u + ((0x3f800003u - b) >> 2);    // k < 0: (3 - k) >> 2
+    return __uint_as_float(b >= 0x3f800000u ? above : below);
+#endif
 }
 // normalize() of a vector that is a unit vector up to rounding (a reflected
 // or negated unit vector): the closed form when every lane's squared length
@@ -1037,7 +1046,13 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         // pow(0, s) is +0 for s > 0 (log2 = -inf, exp2 clamps to 2^-127
         // scaled to 0): skip the polynomials when no lane needs them
         const float xs = gmax(cos_phi, 0.0f);
+#ifdef RT_BRANCHY
         const bool need_pow = !(xs == 0.0f && m.shininess > 0.0f);
+#else
+        // flags combined with & and |, not && and ||: short-circuit evaluation
+        // of LDS-loaded operands compiled to nested divergent branches
+        const bool need_pow = !((xs == 0.0f) & (m.shininess > 0.0f));
+#endif
         float ks = 0.0f;
 #ifdef RT_ABLATE_POW
         ks = xs;
@@ -1051,7 +1066,11 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         // the shadow ray matters only if the light's term can change the sums
         // (host flags, rt_scene.cpp: with a tame material a zero factor or a
         // zero product adds +-0 to sums that are never -0)
+#ifdef RT_BRANCHY
         const bool changes = q.always || (kd != 0.0f && q.d_nz) || (ks != 0.0f && q.s_nz);
+#else
+        const bool changes = (q.always != 0) | ((kd != 0.0f) & (q.d_nz != 0)) | ((ks != 0.0f) & (q.s_nz != 0));
+#endif
         const bool need = valid && changes;
         if (j == 1) RT_PHASE(5);
 #ifdef RT_ABLATE_SHADOW
