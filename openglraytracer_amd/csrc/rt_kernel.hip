@@ -222,7 +222,16 @@ __device__ __forceinline__ float glsl_pow_cos(float x, float y) {
     const float e = static_cast<float>(static_cast<int>((i >> 23) & 0xffu) - 127);
     const float mant = __uint_as_float((i & 0x007fffffu) | 0x3f800000u);
     const float q = div_r(mant - 1.0f, rcp_refined(mant + 1.0f));
+#ifndef RT_POW_SINK
+    // computed in every lane (the empty asm pins the value): left to itself
+    // the compiler sank the polynomial into a divergent branch around the
+    // zero case (configs 3-4 -2 %, config 2 -1 % as a select)
+    float lr = __builtin_fmaf(q, poly_log2(q * q), e);
+    asm volatile("" : "+v"(lr));
+    const float l = x == 0.0f ? -__builtin_inff() : lr;
+#else
     const float l = x == 0.0f ? -__builtin_inff() : __builtin_fmaf(q, poly_log2(q * q), e);
+#endif
     return glsl_exp2(l * y);
 #endif
 }
