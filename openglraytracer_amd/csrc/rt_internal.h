@@ -55,7 +55,9 @@ struct MatRec {
     float amb_sum[4];
     float emissive[4];
     float shininess, reflectivity, transparency, refraction_index;
-};  // 48 B
+    float eta_in, eta_out;  // 1.0 / refraction_index and 1.0 / that (:1013-1016), each correctly rounded
+    float pad[2];
+};  // 64 B
 // The flags decide whether a light's direct term can change the Phong sums;
 // the shadow ray is cast only then (lit and shadowed agree otherwise):
 // d_nz / s_nz: some component of Ld*Md / Ls*Ms is nonzero; always: the

@@ -163,11 +163,21 @@ __device__ __forceinline__ float comp(v3 v, int i) { return i == 0 ? v.x : (i ==
 // reflect(I, N) = I - 2 * dot(N, I) * N
 __device__ __forceinline__ v3 reflect(v3 i, v3 n) { return sub(i, muls(n, 2.0f * dot(n, i))); }
 // refract(I, N, eta) with k = 1 - eta * (eta * (1 - dot^2)) (Mesa's builtin)
+__device__ __forceinline__ float sphere_sqrt(float qd);
 __device__ __forceinline__ v3 refract(v3 i, v3 n, float eta) {
     const float d = dot(n, i);
     const float k = 1.0f - eta * (eta * (1.0f - d * d));
+#ifdef RT_REFRACT_OLD
     if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
     return sub(muls(i, eta), muls(n, eta * d + sqrtf(k)));
+#else
+    // every lane computes the ray (the short square root when every lane's
+    // operand allows it; a total internal reflection lane takes any operand)
+    // and total internal reflection selects the zero vector
+    const bool tir = k < 0.0f;
+    const v3 r = sub(muls(i, eta), muls(n, eta * d + sphere_sqrt(tir ? 1.0f : k)));
+    return tir ? mk(0.0f, 0.0f, 0.0f) : r;
+#endif
 }
 // mix(x, y, a) evaluated as x + a * (y - x)
 __device__ __forceinline__ v3 mix(v3 x, v3 y, float a) { return add(x, muls(sub(y, x), a)); }
@@ -744,6 +754,8 @@ __device__ __forceinline__ int direction_texel(int n, v3 u) {
     const float ua = fx ? u.y : u.x, ub = fy || fx ? u.z : u.y;
     const int face = 2 * (fx ? 0 : (fy ? 1 : 2)) + (um < 0.0f ? 1 : 0);
     const float am = fabsf(um);
+    // (computed in every lane and selected instead of the early return:
+    // measured even, r02k)
     if (!(am > 1e-20f && am < 1e30f)) return -1;
     const float h = 0.5f * static_cast<float>(n) * __builtin_amdgcn_rcpf(am);
     const int col = min(max(static_cast<int>(floorf(ua * h + 0.5f * n)), 0), n - 1);
@@ -1195,8 +1207,12 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
             Frame fr;
             fr.col = col;
             fr.rs = sub(c.p, muls(c.n, 0.001f));
+#ifdef RT_IOR_DIV
             float ratio = 1.0f / m.refraction_index;
             if (c.inside) ratio = 1.0f / ratio;
+#else
+            const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
+#endif
             fr.rd = refract(ray.dir, c.n, ratio);
             fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3);
             F.set(level, fr);
@@ -1327,8 +1343,7 @@ __device__ __forceinline__ v3 trace_tree_u(const Scene &S, Ray ray, bool active)
                 UFrame fr;
                 fr.col = value;
                 fr.rs = sub(c.p, muls(c.n, 0.001f));
-                float ratio = 1.0f / m.refraction_index;
-                if (c.inside) ratio = 1.0f / ratio;
+                const float ratio = c.inside ? m.eta_out : m.eta_in;
                 fr.rd = refract(ray.dir, c.n, ratio);
                 fr.mf = c.material | (on ? kOn : 0) | (sr ? kSr : 0) | (st ? kSt : 0);
                 F.set(level, fr);

@@ -832,6 +832,8 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         r.reflectivity = mats[m].reflectivity;
         r.transparency = mats[m].transparency;
         r.refraction_index = mats[m].refraction_index;
+        r.eta_in = 1.0f / r.refraction_index;  // the ratio of a ray entering (IEEE division, as the kernel's)
+        r.eta_out = 1.0f / r.eta_in;           // and of one leaving the object
         // tame: every product finite and shininess in (0, 1e6): then the
         // diffuse factor max(cos, 0) <= 1 + 2^-20 and pow(max(cos, 0),
         // shininess) are finite (pow is skipped for a zero base; its exp2
