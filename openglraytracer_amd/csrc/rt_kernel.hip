@@ -1171,13 +1171,43 @@ struct Frame {
                   // 48, config 4 18.68 -> 18.26 ms, config 3 1.022 -> 1.000 ms)
 };
 
+#ifdef RT_ABLATE_FRAMES
+// Timing-only ablation (wrong images by design): only the walk's flags are
+// kept (4 bits per level in one register); colours and pending rays are not
+// stored, so the scratch traffic of the frames disappears while the walk
+// visits the same nodes.
 template <int N>
-struct Frames {  // per-level frames, indexed by a per-lane level: the compiler keeps them in
+struct Frames {
+    uint32_t bits = 0;
+    __device__ __forceinline__ Frame get(int level) const {
+        Frame f;
+        f.col = mk(0.0f, 0.0f, 0.0f);
+        f.rs = mk(0.0f, 0.0f, 0.0f);
+        f.rd = mk(0.0f, 0.0f, 1.0f);
+        f.flags = static_cast<int>((bits >> (4 * level)) & 7u);
+        return f;
+    }
+    __device__ __forceinline__ void set(int level, const Frame &v) {
+        bits = (bits & ~(15u << (4 * level))) | ((static_cast<uint32_t>(v.flags) & 7u) << (4 * level));
+    }
+};
+template <int N>
+struct FramesReal {
+#else
+template <int N>
+struct Frames {
+#endif  // per-level frames, indexed by a per-lane level: the compiler keeps them in
                  // scratch; indexed directly, a push or pop moves one 40-B frame (per-level
                  // selects read every level's frame: config 4 18.80 vs 19.08 ms, depth-4
                  // scratch 292 vs 400 B per lane; frames split into colour + flags and
                  // a pending ray stored only when a refraction child waits measured
-                 // slower, config 4 16.93 -> 17.12 ms, config 3 0.933 -> 0.957 ms)
+                 // slower, config 4 16.93 -> 17.12 ms, config 3 0.933 -> 0.957 ms, and
+                 // so did field-by-field access of these 40-B frames, config 4
+                 // 16.62 -> 16.91 ms, config 3 0.921 -> 0.948 ms. What the frames
+                 // cost at most: RT_ABLATE_FRAMES, which keeps only the flags,
+                 // renders config 4 in 11.4 instead of 16.6 ms and config 3 in
+                 // 0.82 instead of 0.92 ms — the latency of the pop's scratch
+                 // load, not the bytes, is the cost)
     Frame f[N];
     __device__ __forceinline__ Frame get(int level) const { return f[level]; }
     __device__ __forceinline__ void set(int level, const Frame &v) { f[level] = v; }
