@@ -1206,8 +1206,8 @@ struct Frames {
                  // 16.62 -> 16.91 ms, config 3 0.921 -> 0.948 ms. What the frames
                  // cost at most: RT_ABLATE_FRAMES, which keeps only the flags,
                  // renders config 4 in 11.4 instead of 16.6 ms and config 3 in
-                 // 0.82 instead of 0.92 ms — the latency of the pop's scratch
-                 // load, not the bytes, is the cost)
+                 // 0.82 instead of 0.92 ms; the top levels in LDS, in 768-thread
+                 // queued groups, measured config 3 -1 %, config 4 +2 %)
     Frame f[N];
     __device__ __forceinline__ Frame get(int level) const { return f[level]; }
     __device__ __forceinline__ void set(int level, const Frame &v) { f[level] = v; }
