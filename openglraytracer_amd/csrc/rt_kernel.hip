@@ -810,6 +810,20 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
             hit = sphere_blocks(qb, qc, qa2, qa4, floor);
         }
     };
+    // the same test for the mask walks, whose candidate words are already
+    // empty for lanes without the query or with a hit
+    auto exact_cand = [&](int s) {
+#ifdef RT_EXACT_GUARD
+        exact(s);
+#else
+        RT_STAT(8, true);
+        const float4 c = S.sph[s];
+        const v3 oc = sub(start, mk(c.x, c.y, c.z));
+        const float qb = dot(d2, oc);
+        const float qc = dot(oc, oc) - c.w;
+        hit = sphere_blocks(qb, qc, qa2, qa4, floor);
+#endif
+    };
     if (!S.cull) {
         for (int s = 0; s < S.ns; ++s) {
             if (!__any(need && !hit)) break;
@@ -846,7 +860,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
             while (__any(cand != 0u)) {
                 RT_STAT(9, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (cand) {
-                    exact(64 * w + __builtin_ctzll(cand));
+                    exact_cand(64 * w + __builtin_ctzll(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
                 }
             }
@@ -862,7 +876,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
             uint64_t cand = need && !hit ? mask : 0u;
             while (__any(cand != 0u)) {
                 if (cand) {
-                    exact(__builtin_ctzll(cand));
+                    exact_cand(__builtin_ctzll(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
                 }
             }
@@ -871,7 +885,7 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
             while (__any(cand != 0u)) {
                 RT_STAT(12, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (cand) {
-                    exact(__builtin_ctz(cand));
+                    exact_cand(__builtin_ctz(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
                 }
             }
