@@ -793,6 +793,44 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
 #ifdef RT_ABLATE_SPHSHADOW
     return hit;
 #endif
+#ifndef RT_SHADOW_EAGER_TERMS
+    if (S.cull && !S.gmask && S.dmask) {
+        // the LDS-mask walk (see below) with the ray's quadratic terms
+        // computed only when some lane of the wave has a candidate (most
+        // shadow queries of a wave have none: config 2 -1 %)
+        const uint64_t m64 = need && !hit ? mask : 0u;
+        if (!__any(m64 != 0u)) return hit;
+        const v3 d2 = muls(dir, 2.0f);
+        const float qa = dot(dir, dir);
+        const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
+        const float floor = root_floor(qa2);
+        const auto test = [&](int s) {
+            RT_STAT(8, true);
+            const float4 c = S.sph[s];
+            const v3 oc = sub(start, mk(c.x, c.y, c.z));
+            hit = sphere_blocks(dot(d2, oc), dot(oc, oc) - c.w, qa2, qa4, floor);
+        };
+        if (S.dmask_bytes == 8) {
+            uint64_t cand = m64;
+            while (__any(cand != 0u)) {
+                if (cand) {
+                    test(__builtin_ctzll(cand));
+                    cand = hit ? 0u : cand & (cand - 1u);
+                }
+            }
+        } else {  // 32-bit masks: half the bit arithmetic
+            uint32_t cand = static_cast<uint32_t>(m64);
+            while (__any(cand != 0u)) {
+                RT_STAT(12, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
+                if (cand) {
+                    test(__builtin_ctz(cand));
+                    cand = hit ? 0u : cand & (cand - 1u);
+                }
+            }
+        }
+        return hit;
+    }
+#endif
     const v3 d2 = muls(dir, 2.0f);
     const float qa = dot(dir, dir);
     const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
