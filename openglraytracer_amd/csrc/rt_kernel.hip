@@ -787,8 +787,16 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     RT_STAT(7, need);
     RT_STAT(10, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
-    for (int b = 0; b < S.nb; ++b)
+    for (int b = 0; b < S.nb; ++b) {
+#ifdef RT_BOX_GUARD
         if (need && !hit) hit = box_occludes(cload(S.cbox + b), start, dir, light_bit);
+#else
+        // every lane tests (no divergent branch around the test; lanes
+        // without the query or already shadowed keep their flag)
+        const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit);
+        hit = hit | (need & occ);
+#endif
+    }
     if (!__any(need && !hit)) return hit;
 #ifdef RT_ABLATE_SPHSHADOW
     return hit;
