@@ -4,21 +4,28 @@ Default workload (BASELINE.json configs[1]):
 1920x1080, room box + 16 seeded spheres, the reference's 3 lights and 7
 materials, max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
 
-config2 (default). A step is the animated frame loop (main.cpp:81-86): F
-frames of 1920x1080 per GPU (--frames-per-gpu, default 8; frame k is the
-reference orbit camera at time k/60 s), rendered up to 8 frames per launch
-(rt_render_batch; SURVEY.md §8(f) row 3 — several frames per launch amortise
-the launch ramp-up and tail). At N=1 the line also carries the one-frame-per-
-launch rate (`single_frame`, the shape of the reference's draw()). On N GPUs
-a step holds N*F frames; the frames of the animated loop are independent
-units, so rank k renders frames [kF, (k+1)F) whole, with no data-path
-collective. Weak scaling. --frame-exchange all_to_all instead row-tiles every
-frame across the N ranks in interleaved 8-row blocks, each rank renders its
-blocks of all N*F frames, and one RCCL all-to-all over xGMI hands frames
-[kF, (k+1)F) to rank k (N gathers at once), which de-interleaves its rows;
-the shards travel as packed float3 (the alpha channel is the constant 0), and
-the exchange of step i runs on its own stream beside the render of step i+1
-(double-buffered).
+config2 (default). A step is F frames of the animated frame loop
+(main.cpp:81-86; --frames, default 8; frame k is the reference orbit camera at
+time k/60 s), rendered up to 8 frames per launch (rt_render_batch; SURVEY.md
+§8(f) row 3 — several frames per launch amortise the launch ramp-up and
+tail). The total work of a step is fixed: strong scaling.
+  * N=1: every frame whole, float4 per pixel (16 B: the HBM-write roofline's
+    bytes). The line also carries the one-frame-per-launch rate
+    (`single_frame`, the shape of the reference's draw(), main.cpp:228-238).
+  * N>1 (north_star: "image row-tiles shard across the GPUs with an RCCL
+    gather over xGMI to assemble the frame"): every frame is row-tiled over
+    the N ranks in interleaved 8-row blocks; each rank renders its blocks of
+    all F frames (rt_render_batch with shards), one RCCL gather per step
+    brings the shards to rank 0, which de-interleaves them into the F frames;
+    the gather of step i overlaps the render of step i+1 (double-buffered).
+    The shards travel in the shipped app's GL_RGBA8 surface format
+    (main.cpp:152-159, :223; RT_OUTPUT_RGBA8, byte-exact vs the reference's
+    GL render): 4 B per pixel instead of 16 — 8.3 MB per 1080p frame through
+    rank 0's xGMI ingress. The line also carries `independent_frames`: every
+    rank renders F whole frames of its own with no collective (weak scaling),
+    and `verified`: the assembled frames of the last step equal rank 0's own
+    whole-frame render byte for byte. --frame-exchange all_to_all instead
+    hands frame k to rank k (N gathers at once); none = independent frames.
 
 config3 / config4 (3840x2160 / 64 spheres / depth 2, and
 7680x4320 / 256 spheres / depth 4 row-tiled across the GPUs with an RCCL
@@ -26,8 +33,7 @@ gather). A step is ONE frame. N=1 renders it whole (float4). N>1: the frame's
 interleaved 8-row blocks are dealt round-robin to the ranks (rt_render_shard,
 packed float3 shards), one RCCL gather brings the shards to rank 0 and rank 0
 de-interleaves them into the frame (frame.gather_frame); the gather of step i
-overlaps the render of step i+1. Strong scaling. The line reports every
-rank's kernel time and the gather and assembly times separately.
+overlaps the render of step i+1. Strong scaling, verified like config2.
 
 config5 (a Monte-Carlo extension the reference does not have): one step =
 the 1920x1080 frame at 1024 jittered samples per pixel, samples sharded over
@@ -36,10 +42,12 @@ value = samples/s.
 
 value = primary rays (samples) of the step / step time (max over ranks), Mrays/s.
 roofline = the render kernel against the HBM-write roofline: bytes stored per
-launch (16 B per pixel for a float4 frame, 12 for float3 shards) / average
-kernel time from HIP events on the launch stream (config2 at N=1: one pair
-around the K back-to-back launches of the timed region; otherwise a pair
-around every step's launches).
+launch (16 B per pixel for a float4 frame, 12 for float3 shards, 4 for RGBA8)
+/ average kernel time from HIP events on the launch stream (one pair around
+the back-to-back launches of the timed region when a step has no collective;
+otherwise a pair around every step's launches). Its `traffic` and `valu`
+come from the committed rocprofv3 PMC summary of the same sources
+(profiles/pmc_<workload>_latest.json), else they say which build they belong to.
 cpu_baseline = the reference's own shader on Mesa llvmpipe (oracle/_ref) on the
 host cores, median of 3 dispatches, plus a 1-thread sample and the other
 configs' row subsets (oracle/cpu_baseline.py, child process, N=1 only).
@@ -49,6 +57,7 @@ configs' row subsets (oracle/cpu_baseline.py, child process, N=1 only).
 import argparse
 import json
 import os
+import re
 import subprocess
 import sys
 import time
@@ -80,12 +89,19 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
-    ap.add_argument("--frames-per-gpu", type=int, default=8,
-                    help="config2: animated frames each GPU renders per step, up to 8 per launch "
-                         "(rt_render_batch; SURVEY.md §8(f) row 3)")
-    ap.add_argument("--frame-exchange", choices=["none", "all_to_all"], default="none",
-                    help="config2 at N>1: none = every rank renders whole frames of its own; all_to_all = "
-                         "every frame row-tiled over the ranks and exchanged (frame k gathered to rank k)")
+    ap.add_argument("--frames", type=int, default=8,
+                    help="config2: animated frames per step, up to 8 per launch (rt_render_batch; "
+                         "SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
+    ap.add_argument("--frame-exchange", choices=["gather", "all_to_all", "none"], default="gather",
+                    help="config2 at N>1: gather = every frame row-tiled over the ranks and gathered to rank 0 "
+                         "(north_star); all_to_all = frame k gathered to rank k; none = every rank renders "
+                         "whole frames of its own")
+    ap.add_argument("--surface", choices=["auto", "rgba32f", "rgba8"], default="auto",
+                    help="config2 surface: auto = float4 at N=1, the GL_RGBA8 surface for row-tiled frames at N>1")
+    ap.add_argument("--no-independent", action="store_true",
+                    help="config2 at N>1: skip the secondary independent-frames measurement")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="N>1: skip checking the assembled frames against rank 0's whole-frame render")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,19 +131,30 @@ def cpu_baseline(workload, budget_s):
     return None
 
 
-def pmc_latest(workload, frames_per_launch):
+def source_id(build):
+    """The source hash of a build string (rt_version(): '... (gfx950, src
+    <hash>, git <rev>)'), or the whole string for older builds."""
+    m = re.search(r"src ([0-9a-f]+)", build or "")
+    return m.group(1) if m else (build or "")
+
+
+def pmc_latest(workload, frames_per_launch, build):
     """The committed PMC summary of the render kernel for this workload and
     launch shape at N=1 (profiles/pmc_<workload>_latest.json, written by
-    tools/pmc_summary.py; config2 also profiles/pmc_latest.json), or {}."""
+    tools/pmc_summary.py; config2 also profiles/pmc_latest.json), or {}.
+    A summary profiled on a build with other sources is returned only as
+    {"stale_build": ...}: its counters are not this kernel's."""
     for name in ("pmc_%s_latest.json" % workload, "pmc_latest.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 d = json.load(f)
-            if (d.get("workload") == workload and d.get("n_gpus", 1) == 1
-                    and d.get("frames_per_launch", 1) == frames_per_launch):
-                return d
         except (OSError, ValueError):
-            pass
+            continue
+        if (d.get("workload") == workload and d.get("n_gpus", 1) == 1
+                and d.get("frames_per_launch", 1) == frames_per_launch):
+            if source_id(d.get("build")) != source_id(build):
+                return {"stale_build": d.get("build"), "profile": name}
+            return d
     return {}
 
 
@@ -135,6 +162,9 @@ def valu_bound(pmc, kernel_ms):
     """The bound the kernel actually sits against: VALU issue.
     Peak = one wave64 VALU instruction per 2 cycles per SIMD (SIMD-32),
     1024 SIMDs at 2.4 GHz (/opt/skills/guides/MI355X_MICROARCH.md)."""
+    if "stale_build" in pmc:
+        return {"stale_build": pmc["stale_build"], "note": "profiles/%s was measured on other sources; "
+                "no VALU figure for this build" % pmc["profile"]}
     insts = pmc.get("sq_insts_valu_per_launch")
     if not insts or kernel_ms <= 0:
         return None
@@ -142,10 +172,14 @@ def valu_bound(pmc, kernel_ms):
     achieved = insts / (kernel_ms * 1e-3) / 1e12
     out = {"wave_insts_per_launch": insts, "achieved": round(achieved, 4), "peak": round(peak, 4),
            "unit": "T wave-instr/s", "frac": round(achieved / peak, 4),
-           "source": "SQ_INSTS_VALU from profiles/pmc_*_latest.json (rocprofv3 --pmc pass of the build "
-                     "committed before this run: %s)" % pmc.get("build", "?")}
+           "source": "SQ_INSTS_VALU from profiles/pmc_*_latest.json (rocprofv3 --pmc pass of this build: %s)"
+                     % pmc.get("build", "?")}
     if pmc.get("scratch_bytes_per_lane") is not None:
         out["scratch_bytes_per_lane"] = pmc["scratch_bytes_per_lane"]
+    if pmc.get("effective_clock_ghz"):
+        clk = pmc["effective_clock_ghz"]
+        out["frac_at_measured_clock"] = round(insts * 2 / (1024 * clk * 1e9 * kernel_ms * 1e-3), 4)
+        out["measured_clock_ghz"] = round(clk, 3)
     return out
 
 
@@ -163,6 +197,25 @@ class Timer:
 
     def ms(self):
         return [a.elapsed_time(b) for a, b in self.ev]
+
+
+class Plan:
+    """One measured step shape: what a step renders (on the render stream),
+    how the shards are exchanged and assembled (on the collective stream)."""
+
+    def __init__(self, bufs, render, rays_per_step, px_per_launch, bytes_per_pixel, launches_per_step=1,
+                 collective=None, assemble=None, per_launch=True):
+        self.bufs = bufs
+        self.render = render            # render(buf), asynchronous on the render stream
+        self.collective = collective    # collective(slot, src): on the collective stream after slot's render
+        self.assemble = assemble        # assemble(slot): on the collective stream after the collective
+        self.rays_per_step = rays_per_step
+        self.px_per_launch = px_per_launch
+        self.bytes_per_pixel = bytes_per_pixel
+        self.launches_per_step = launches_per_step
+        # one kernel event pair per step (else one pair around the timed region)
+        self.per_launch = per_launch or collective is not None
+        self.last = None                # assembled output of the last step (assemble's return value)
 
 
 def main():
@@ -205,103 +258,143 @@ def main():
     assert sh, "need a non-default HIP stream"
     wl = args.workload
     mc = wl == "config5"
-    batched = wl == "config2"  # N*F frames per step in batched launches
-    exchange = batched and world > 1 and args.frame_exchange == "all_to_all"
-    sharded = world > 1 and not mc and (exchange or not batched)  # ranks render row-tiles of shared frames
-    channels = 3 if sharded else 4
-    bytes_per_pixel = 4 * channels  # the render's store per pixel (algorithmic HBM bytes)
-    if channels == 3:
-        ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
+    batched = wl == "config2"
+    F = args.frames
     extra = {}
+    surfaces = {"rgba32f": (rt.abi.RT_OUTPUT_RGBA32F, 4, torch.float32, "float4"),
+                "rgb32f": (rt.abi.RT_OUTPUT_RGB32F, 3, torch.float32, "packed float3 (alpha 0 dropped)"),
+                "rgba8": (rt.abi.RT_OUTPUT_RGBA8, 1, torch.int32, "GL_RGBA8 surface (4 B per pixel)")}
 
-    if batched and not exchange:
-        # N*F frames in flight, frame k = the orbit camera at t = k/60 s;
-        # rank r renders frames [rF, (r+1)F) whole, up to 8 per launch
-        # (rt_render_batch), in place, launches back to back.
-        fpg = args.frames_per_gpu
-        n_frames = fpg
-        views = [rt.make_view(None, frame_time(rank * fpg + k)) for k in range(fpg)]
-        bufs = [torch.zeros(fpg * H * W * 4, dtype=torch.float32, device="cuda")]
-        chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, fpg, rt.abi.RT_MAX_BATCH)]
-        frame_elems = H * W * 4
-        launches_per_step = len(chunks)
-        px_per_launch = W * H * fpg // launches_per_step
-        rays_per_step = world * fpg * W * H
+    def surface(name):
+        fmt, ch, dt, text = surfaces[name]
+        ctx.set_output(fmt)
+        return ch, dt, text
 
-        def render(buf):
-            for j, vs in chunks:
-                rt.render_batch(ctx, scene, buf.data_ptr() + 4 * j * frame_elems, W, H, DEPTH, vs, stream=sh)
-    elif batched:
-        # N frames in flight, frame k = the orbit camera at t = k/60 s; every
-        # rank renders its interleaved 8-row blocks of all N frames in one
-        # launch (rt_render_batch); one all-to-all hands frame k's rows to
-        # rank k (N gathers at once), which de-interleaves its frame. Double
-        # buffered: the exchange of step i overlaps the render of step i+1.
-        fpg = args.frames_per_gpu
-        n_frames = world * fpg
+    def batch_plan(mode, surf):
+        """config2: F frames per step (per rank for `none`, all_to_all),
+        rendered up to 8 per launch; see the module docstring."""
+        ch, dt, _ = surface(surf)
+        esize = 4  # bytes per element (float32 / int32)
+        if mode == "none" or world == 1:
+            # frames [rF, (r+1)F) whole on rank r, in place, launches back to back
+            views = [rt.make_view(None, frame_time(rank * F + k)) for k in range(F)]
+            bufs = [torch.zeros(F * H * W * ch, dtype=dt, device="cuda")]
+            chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, F, rt.abi.RT_MAX_BATCH)]
+
+            def render(buf):
+                for j, vs in chunks:
+                    rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * H * W * ch, W, H, DEPTH, vs, stream=sh)
+            return Plan(bufs, render, world * F * W * H, W * H * F // len(chunks), esize * ch, len(chunks),
+                        per_launch=False)
+        n_frames = F if mode == "gather" else world * F
         views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
-        rows_mine = H if world == 1 else rt.shard_rows(H, BLOCK_ROWS, world, rank)
-        bufs = [torch.zeros(n_frames * rows_mine * W * channels, dtype=torch.float32, device="cuda")
-                for _ in range(2 if world > 1 else 1)]
+        rows_mine = rt.shard_rows(H, BLOCK_ROWS, world, rank)
+        if mode == "gather":
+            elems = frame.flat_shard_elems(n_frames, H, W, BLOCK_ROWS, world, ch)
+        else:
+            elems = n_frames * rows_mine * W * ch
+        bufs = [torch.zeros(elems, dtype=dt, device="cuda") for _ in range(2)]
         chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, n_frames, rt.abi.RT_MAX_BATCH)]
-        frame_elems = rows_mine * W * channels
-        if world > 1:
-            in_splits, out_splits = frame.exchange_splits(H, W, BLOCK_ROWS, world, rank, channels=channels,
-                                                          frames_per_rank=fpg)
-            recv = [torch.empty(sum(out_splits), dtype=torch.float32, device=coll_dev) for _ in bufs]
-            idx = torch.as_tensor(frame.assembly_rows(H, BLOCK_ROWS, world, fpg), device=coll_dev)
-        launches_per_step = len(chunks)
-        px_per_launch = W * rows_mine * n_frames // launches_per_step
-        rays_per_step = n_frames * W * H
+        frame_elems = rows_mine * W * ch
 
         def render(buf):
             for j, vs in chunks:
-                rt.render_batch(ctx, scene, buf.data_ptr() + 4 * j * frame_elems, W, H, DEPTH, vs,
+                rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * frame_elems, W, H, DEPTH, vs,
                                 BLOCK_ROWS, world, rank, stream=sh)
-    elif mc:
-        view = rt.make_view(None, 0.0)
-        spp = cfg["spp"]
-        spp_mine = spp // world + (1 if rank < spp % world else 0)
-        sample0 = rank * (spp // world) + min(rank, spp % world)
-        accum = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-        px_per_launch = W * H
-        rays_per_step = spp * W * H
-        launches_per_step = 1
-    else:
-        # one frame per step: whole at N=1, row-tiled + gathered at N>1
-        view = rt.make_view(None, 0.0)
-        rows_mine = H if world == 1 else rt.shard_rows(H, BLOCK_ROWS, world, rank)
-        shard_elems = frame.flat_shard_elems(1, H, W, BLOCK_ROWS, world, channels) if world > 1 else H * W * 4
-        bufs = [torch.zeros(shard_elems, dtype=torch.float32, device="cuda") for _ in range(2 if world > 1 else 1)]
-        if world > 1 and rank == 0:
-            glists = [[torch.empty(shard_elems, dtype=torch.float32, device=coll_dev) for _ in range(world)]
-                      for _ in bufs]
+        if mode == "gather":
+            glists = ([[torch.empty(elems, dtype=dt, device=coll_dev) for _ in range(world)] for _ in bufs]
+                      if rank == 0 else None)
             perm = torch.as_tensor(frame.assembly_permutation(H, BLOCK_ROWS, world), device=coll_dev)
-        launches_per_step = 1
-        px_per_launch = W * rows_mine
-        rays_per_step = W * H
 
-        def render(buf):
-            if world == 1:
-                rt.render_device(ctx, scene, buf.data_ptr(), W, H, DEPTH, view=view, stream=sh)
-            else:
-                rt.render_shard(ctx, scene, buf.data_ptr(), W, H, DEPTH, BLOCK_ROWS, world, rank, view=view,
-                                stream=sh)
+            def collective(slot, src):
+                dist.gather(src, glists[slot] if rank == 0 else None, dst=0)  # RCCL: every shard to rank 0
 
-    # Kernel time from HIP events on the render stream. config2 without an
-    # exchange: a step is its render launches alone, one event pair brackets
-    # the back-to-back launches of the whole timed region (no markers between
-    # frames); otherwise a pair brackets every step's render launches.
-    per_launch = not (batched and not exchange)
-    kt = Timer(torch, args.steps if per_launch else 1)
-    ct = Timer(torch, args.steps)  # collective (exchange / gather / all-reduce) on comm_s
-    at = Timer(torch, args.steps)  # frame assembly on comm_s (rank 0 / every rank for the exchange)
-    rendered = [torch.cuda.Event() for _ in range(2)]
-    freed = [None, None]  # event: the collective has finished reading bufs[slot]
-    state = {"collective": False}
+            def assemble(slot):
+                if rank == 0:  # de-interleave the row blocks into the F frames
+                    return frame.assemble(glists[slot], n_frames, H, W, BLOCK_ROWS, channels=ch, perm=perm)
+                return None
+        else:
+            in_splits, out_splits = frame.exchange_splits(H, W, BLOCK_ROWS, world, rank, channels=ch,
+                                                          frames_per_rank=F)
+            recv = [torch.empty(sum(out_splits), dtype=dt, device=coll_dev) for _ in bufs]
+            idx = torch.as_tensor(frame.assembly_rows(H, BLOCK_ROWS, world, F), device=coll_dev)
 
-    def step(timed, it=0):
-        if mc:
+            def collective(slot, src):
+                dist.all_to_all_single(recv[slot], src, out_splits, in_splits)  # frames [kF, (k+1)F) -> rank k
+
+            def assemble(slot):
+                return frame.assemble_frames(recv[slot], F, H, W, BLOCK_ROWS, world, channels=ch, idx=idx)
+        return Plan(bufs, render, n_frames * W * H, W * rows_mine * n_frames // len(chunks), esize * ch,
+                    len(chunks), collective, assemble)
+
+    def frame_plan():
+        """config3 / config4: one frame per step, whole at N=1, row-tiled +
+        gathered at N>1."""
+        ch, dt, _ = surface("rgba32f" if world == 1 else "rgb32f")
+        view = rt.make_view(None, 0.0)
+        if world == 1:
+            bufs = [torch.zeros(H * W * 4, dtype=dt, device="cuda")]
+            return Plan(bufs, lambda buf: rt.render_device(ctx, scene, buf.data_ptr(), W, H, DEPTH, view=view,
+                                                           stream=sh), W * H, W * H, 16)
+        rows_mine = rt.shard_rows(H, BLOCK_ROWS, world, rank)
+        elems = frame.flat_shard_elems(1, H, W, BLOCK_ROWS, world, ch)
+        bufs = [torch.zeros(elems, dtype=dt, device="cuda") for _ in range(2)]
+        glists = ([[torch.empty(elems, dtype=dt, device=coll_dev) for _ in range(world)] for _ in bufs]
+                  if rank == 0 else None)
+        perm = torch.as_tensor(frame.assembly_permutation(H, BLOCK_ROWS, world), device=coll_dev)
+
+        def collective(slot, src):
+            dist.gather(src, glists[slot] if rank == 0 else None, dst=0)  # RCCL: every shard to rank 0
+
+        def assemble(slot):
+            if rank == 0:
+                return frame.assemble(glists[slot], 1, H, W, BLOCK_ROWS, channels=ch, perm=perm)
+            return None
+        return Plan(bufs, lambda buf: rt.render_shard(ctx, scene, buf.data_ptr(), W, H, DEPTH, BLOCK_ROWS, world,
+                                                      rank, view=view, stream=sh),
+                    W * H, W * rows_mine, 4 * ch, 1, collective, assemble)
+
+    def measure(plan, steps, warmup):
+        """Warm-up, then `steps` timed steps between barriers; returns the
+        elapsed seconds (max over ranks) and mean kernel / collective /
+        assembly ms of every rank."""
+        kt = Timer(torch, steps if plan.per_launch else 1)
+        ct = Timer(torch, steps)  # collective on comm_s
+        at = Timer(torch, steps)  # assembly on comm_s
+        rendered = [torch.cuda.Event() for _ in plan.bufs]
+        freed = [None] * len(plan.bufs)  # event: the collective has finished reading bufs[slot]
+
+        def step(timed, it):
+            if not plan.per_launch:  # frames rendered in place, launches back to back
+                plan.render(plan.bufs[0])
+                return
+            slot = it % len(plan.bufs)
+            if freed[slot] is not None:
+                render_s.wait_event(freed[slot])  # the collective of step it-2 has read bufs[slot]
+            if timed:
+                kt.start(it, render_s)
+            plan.render(plan.bufs[slot])
+            if timed:
+                kt.stop(it, render_s)
+            if plan.collective is None:
+                return
+            rendered[slot].record(render_s)
+            comm_s.wait_event(rendered[slot])
+            src = plan.bufs[slot] if coll_dev == "cuda" else plan.bufs[slot].cpu()
+            if timed:
+                ct.start(it, comm_s)
+            plan.collective(slot, src)
+            if timed:
+                ct.stop(it, comm_s)
+                at.start(it, comm_s)
+            plan.last = plan.assemble(slot)
+            if timed:
+                at.stop(it, comm_s)
+            e = torch.cuda.Event()
+            e.record(comm_s)
+            freed[slot] = e
+
+        def mc_step(timed, it):
             accum.zero_()  # on comm_s: after the previous step's all-reduce read it
             render_s.wait_stream(comm_s)
             if timed:
@@ -316,7 +409,6 @@ def main():
             if world > 1:
                 total = accum if coll_dev == "cuda" else accum.cpu()
                 dist.all_reduce(total)  # RCCL: the partial sums of all ranks' samples
-                state["collective"] = True
             else:
                 total = accum
             if timed:
@@ -326,92 +418,115 @@ def main():
                 total.mul_(1.0 / spp)  # the estimate: mean over all samples
             if timed:
                 at.stop(it, comm_s)
-            return
-        if not per_launch:  # config2 without exchange: frames rendered in place, launches back to back
-            render(bufs[0])
-            return
-        slot = it % 2 if world > 1 else 0
-        if freed[slot] is not None:
-            render_s.wait_event(freed[slot])  # the collective of step it-2 has read bufs[slot]
-        if timed:
-            kt.start(it, render_s)
-        render(bufs[slot])
-        if timed:
-            kt.stop(it, render_s)
-        if world == 1:
-            return
-        rendered[slot].record(render_s)
-        comm_s.wait_event(rendered[slot])
-        src = bufs[slot] if coll_dev == "cuda" else bufs[slot].cpu()
-        if timed:
-            ct.start(it, comm_s)
-        if exchange:
-            dist.all_to_all_single(recv[slot], src, out_splits, in_splits)  # frames [kF, (k+1)F) -> rank k
-            if timed:
-                ct.stop(it, comm_s)
-                at.start(it, comm_s)
-            frame.assemble_frames(recv[slot], fpg, H, W, BLOCK_ROWS, world, channels=channels, idx=idx)
-        else:
-            if rank == 0:
-                dist.gather(src, glists[slot], dst=0)  # RCCL: every shard to rank 0
-            else:
-                dist.gather(src, None, dst=0)
-            if timed:
-                ct.stop(it, comm_s)
-                at.start(it, comm_s)
-            if rank == 0:  # de-interleave the row blocks into the frame
-                frame.assemble(glists[slot], 1, H, W, BLOCK_ROWS, channels=channels, perm=perm)
-        if timed:
-            at.stop(it, comm_s)
-        state["collective"] = True
-        e = torch.cuda.Event()
-        e.record(comm_s)
-        freed[slot] = e
 
-    for i in range(args.warmup):
-        step(False, i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if not per_launch:
-        kt.start(0, render_s)
-    for it in range(args.steps):
-        step(True, it)
-    if not per_launch:
-        kt.stop(0, render_s)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kernel_ms = ([m / launches_per_step for m in kt.ms()] if per_launch else
-                 [kt.ms()[0] / (args.steps * launches_per_step)])
-    avg_kernel_ms = float(np.mean(kernel_ms))
-    coll_ms = float(np.mean(ct.ms())) if (sharded or mc) else 0.0
-    asm_ms = float(np.mean(at.ms())) if (sharded or mc) else 0.0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        mine = torch.tensor([avg_kernel_ms, coll_ms, asm_ms], dtype=torch.float64, device=coll_dev)
-        every = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(every, mine)
-        per_rank = [[round(float(v), 5) for v in e.cpu().tolist()] for e in every]
+        run = mc_step if mc else step
+        for i in range(warmup):
+            run(False, i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if not plan.per_launch:
+            kt.start(0, render_s)
+        for it in range(steps):
+            run(True, it)
+        if not plan.per_launch:
+            kt.stop(0, render_s)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kernel_ms = ([m / plan.launches_per_step for m in kt.ms()] if plan.per_launch else
+                     [kt.ms()[0] / (steps * plan.launches_per_step)])
+        kms = float(np.mean(kernel_ms))
+        exchanged = mc or plan.collective is not None
+        cms = float(np.mean(ct.ms())) if exchanged else 0.0
+        ams = float(np.mean(at.ms())) if exchanged else 0.0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            mine = torch.tensor([kms, cms, ams], dtype=torch.float64, device=coll_dev)
+            every = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(every, mine)
+            per_rank = [[round(float(v), 5) for v in e.cpu().tolist()] for e in every]
+        else:
+            per_rank = [[round(kms, 5), round(cms, 5), round(ams, 5)]]
+        return elapsed, kms, per_rank
+
+    def verify(plan, n_frames, times, ch, dt, frames_of_rank=None):
+        """The assembled frames of the last step against this rank's own
+        whole-frame renders in the same surface format, byte for byte; the
+        mismatch count is summed over the ranks that assemble."""
+        bad, px = 0, 0
+        if plan.last is not None:
+            got = plan.last.reshape(n_frames, H, W, ch)
+            ref = torch.zeros((n_frames, H, W, ch), dtype=dt, device="cuda")
+            views = [rt.make_view(None, t) for t in times]
+            for j in range(0, n_frames, rt.abi.RT_MAX_BATCH):
+                rt.render_batch(ctx, scene, ref[j].data_ptr(), W, H, DEPTH, views[j:j + rt.abi.RT_MAX_BATCH])
+            torch.cuda.synchronize()
+            diff = (got.to(ref.device) != ref).reshape(n_frames * H * W, ch).any(-1)
+            bad, px = int(diff.sum().item()), n_frames * H * W
+        if world > 1:
+            t = torch.tensor([bad, px], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t)
+            bad, px = int(t[0].item()), int(t[1].item())
+        return {"frames_checked": px // (H * W), "pixels": px, "mismatched_pixels": bad, "bit_exact": bad == 0,
+                "against": "rank 0's own whole-frame render of the same frames, same surface"}
+
+    view = None
+    if batched:
+        mode = args.frame_exchange if world > 1 else "none"
+        surf = args.surface if args.surface != "auto" else ("rgba8" if world > 1 and mode != "none" else "rgba32f")
+        plan = batch_plan(mode, surf)
+    elif mc:
+        view = rt.make_view(None, 0.0)
+        spp = cfg["spp"]
+        spp_mine = spp // world + (1 if rank < spp % world else 0)
+        sample0 = rank * (spp // world) + min(rank, spp % world)
+        accum = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        plan = Plan([accum], None, spp * W * H, W * H, 16)
     else:
-        per_rank = [[round(avg_kernel_ms, 5), coll_ms, asm_ms]]
+        plan = frame_plan()
+
+    elapsed, avg_kernel_ms, per_rank = measure(plan, args.steps, args.warmup)
+    verified = None
+    if world > 1 and not args.no_verify and not mc:
+        if batched and mode == "gather":
+            verified = verify(plan, F, [frame_time(k) for k in range(F)], surfaces[surf][1], surfaces[surf][2])
+        elif batched and mode == "all_to_all":
+            verified = verify(plan, F, [frame_time(rank * F + k) for k in range(F)], surfaces[surf][1],
+                              surfaces[surf][2])
+        elif not batched:
+            ch, dt, _ = surfaces["rgb32f"][1:]
+            ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
+            verified = verify(plan, 1, [0.0], ch, dt)
+    if batched and world > 1 and mode != "none" and not args.no_independent:
+        # secondary: every rank renders F whole frames of its own, no collective
+        ind = batch_plan("none", "rgba32f")
+        e2, k2, r2 = measure(ind, args.steps, args.warmup)
+        extra["independent_frames"] = {
+            "value": round(ind.rays_per_step * args.steps / e2 / 1e6, 3), "unit": "Mrays/s",
+            "ms_per_step": round(e2 / args.steps * 1e3, 5), "frames_per_step": world * F, "frames_per_gpu": F,
+            "scaling": "weak", "output": "float4 frames",
+            "parallelism": "whole frames x%d (rank r renders frames [rF, (r+1)F) of the animated loop), "
+                           "no collective" % world,
+            "kernel_ms_per_rank": [v[0] for v in r2]}
+        del ind
     if batched and world == 1 and rank == 0 and not args.no_single_frame:
         # one frame per launch (the shape of the reference's draw(),
         # main.cpp:210-238): K launches back to back, one event pair
         n1 = max(20, args.steps)
         one = torch.empty(H * W * 4, dtype=torch.float32, device="cuda")
+        views1 = [rt.make_view(None, frame_time(k)) for k in range(F)]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for k in range(3):
-            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views[k % len(views)]], stream=sh)
+            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views1[k % F]], stream=sh)
         e0.record(render_s)
         for k in range(n1):
-            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views[k % len(views)]], stream=sh)
+            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views1[k % F]], stream=sh)
         e1.record(render_s)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n1 * 1e3
@@ -419,38 +534,50 @@ def main():
                                  "value": round(W * H / us, 3), "unit": "Mrays/s",
                                  "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
     ms_per_step = elapsed / args.steps * 1e3
-    value = rays_per_step * args.steps / elapsed / 1e6
-    achieved = px_per_launch * bytes_per_pixel / (avg_kernel_ms * 1e-3) / 1e9
-    fpl = 1 if not batched else n_frames // launches_per_step
-    pmc = pmc_latest(wl, fpl) if world == 1 else {}
+    value = plan.rays_per_step * args.steps / elapsed / 1e6
+    achieved = plan.px_per_launch * plan.bytes_per_pixel / (avg_kernel_ms * 1e-3) / 1e9
+    fpl = plan.px_per_launch // (W * H) if batched and world == 1 else 1
+    build = rt.lib().rt_version().decode()
+    pmc = pmc_latest(wl, fpl, build) if world == 1 else {}
     traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(wl, args.cpu_seconds)
         workload = {"workload": cfg["text"], "width": W, "height": H, "spheres": cfg["spheres"], "max_depth": DEPTH}
-        if batched and not exchange:
-            workload.update({"frames_per_step": world * fpg, "frames_per_gpu": fpg, "frames_per_launch": fpl,
+        collective = "none"
+        if batched and (world == 1 or mode == "none"):
+            workload.update({"frames_per_step": world * F, "frames_per_gpu": F, "frames_per_launch": fpl,
                              "output": "float4 frames",
                              "parallelism": ("whole frames x%d (rank r renders frames [rF, (r+1)F) of the "
                                              "animated loop), no collective" % world) if world > 1
                                             else "single GPU"})
+        elif batched and mode == "gather":
+            collective = "gather to rank 0 (one per step: the shards of all F frames)"
+            workload.update({"frames_per_step": F, "frames_per_launch": min(F, rt.abi.RT_MAX_BATCH),
+                             "row_block": BLOCK_ROWS, "output": surfaces[surf][3] + " shards gathered to rank 0",
+                             "parallelism": "every frame row-tiled x%d in interleaved %d-row blocks + RCCL gather "
+                                            "to rank 0, de-interleaved there, overlapped with the next render"
+                                            % (world, BLOCK_ROWS)})
         elif batched:
-            workload.update({"frames_per_step": n_frames, "frames_per_gpu": fpg,
-                             "frames_per_launch": fpl, "row_block": BLOCK_ROWS,
-                             "output": "float3 shards (alpha 0 dropped) exchanged",
-                             "parallelism": ("row-tiles x%d + RCCL all-to-all frame exchange (frame k gathered to "
-                                             "rank k), overlapped with the next render" % world)
-                                            if world > 1 else "single GPU"})
+            collective = "all_to_all_single (N frame gathers at once)"
+            workload.update({"frames_per_step": world * F, "frames_per_gpu": F,
+                             "frames_per_launch": min(world * F, rt.abi.RT_MAX_BATCH), "row_block": BLOCK_ROWS,
+                             "output": surfaces[surf][3] + " shards exchanged",
+                             "parallelism": "row-tiles x%d + RCCL all-to-all frame exchange (frame k gathered "
+                                            "to rank k), overlapped with the next render" % world})
         elif mc:
+            collective = "all_reduce of the sample sums" if world > 1 else "none"
             workload.update({"spp": cfg["spp"],
                              "parallelism": ("samples x%d + RCCL all-reduce" % world) if world > 1 else "single GPU"})
         else:
+            collective = "gather to rank 0" if world > 1 else "none"
             workload.update({"frames_per_step": 1, "row_block": BLOCK_ROWS,
                              "output": "float4 frame" if world == 1 else
                              "float3 shards (alpha 0 dropped) gathered to rank 0, de-interleaved there",
                              "parallelism": ("interleaved 8-row blocks x%d + RCCL gather to rank 0, overlapped "
                                              "with the next render" % world) if world > 1 else "single GPU"})
+        strong = not (batched and world > 1 and mode in ("none", "all_to_all"))
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -460,7 +587,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak" if batched else "strong",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded scene, SURVEY.md §8(d) %s)" % wl,
@@ -469,25 +596,30 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_ms, 5),
-                         "bytes_per_launch": px_per_launch * bytes_per_pixel,
+                         "bytes_per_launch": plan.px_per_launch * plan.bytes_per_pixel,
                          "valu": valu_bound(pmc, avg_kernel_ms)},
             "timing": {"per_rank": [{"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2]}
                                     for r, v in enumerate(per_rank)],
-                       "collective": {"config2": "all_to_all_single (N frame gathers at once)",
-                                      "config5": "all_reduce of the sample sums"}.get(
-                                          wl, "gather to rank 0") if (sharded or mc) and world > 1 else "none",
+                       "collective": collective,
                        "note": "HIP events: kernel on the render stream, collective and assembly on the "
                                "collective stream, means over the timed steps"},
             "cpu_baseline": cpu,
-            "build": rt.lib().rt_version().decode(),
+            "build": build,
         }
+        if "stale_build" in pmc:
+            line["roofline"]["traffic_note"] = "profiles/%s is of other sources (%s)" % (pmc["profile"],
+                                                                                      pmc["stale_build"])
+        if verified is not None:
+            line["verified"] = verified
         line.update(extra)
         print(json.dumps(line), flush=True)
     scene.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
-
+    if verified is not None and not verified["bit_exact"]:
+        raise SystemExit("assembled frames differ from the whole-frame render on %d pixels"
+                         % verified["mismatched_pixels"])
 
 if __name__ == "__main__":
     main()

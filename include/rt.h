@@ -90,9 +90,13 @@ typedef struct rt_camera {
 
 /* The per-frame camera constants the kernel consumes: the column-major
  * inverse(proj * view) that unprojects NDC (:383) and the ray origin, the
- * camera position (:391). rt_make_view derives it from an rt_camera in
- * float64 (rounded once to float32); callers may also supply their own
- * (e.g. a value another renderer computed). */
+ * camera position (:391). rt_make_view(NULL, time) — the reference's orbit
+ * camera, and what rt_render(cam = NULL) uses — evaluates them in float32
+ * exactly as the reference's GL (llvmpipe) does (rt_camera.cpp; bit-exact vs
+ * tests/golden/camera_llvmpipe.npz); an explicit rt_camera, which the
+ * reference does not have, is evaluated in float64 and rounded once to
+ * float32. Callers may also supply their own (e.g. a value another renderer
+ * computed). */
 typedef struct rt_view {
     float unprojection[16];
     float origin[3];
@@ -165,12 +169,14 @@ void rt_destroy(rt_context *ctx);
 #define RT_MAX_MATERIALS 256
 int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt_material *mats,
                     int n_mats, const rt_light *lights, int n_lights, rt_scene **out);
+/* Frees the scene's device memory in stream order behind every render that
+ * reads it — on the context's stream and on any caller stream (an event per
+ * stream is recorded at each render); no device-wide synchronisation. */
 void rt_scene_destroy(rt_scene *scene);
 /* Replace the scene's contents in place (an animated frame: the reference
  * recomputes its objects from `time` every frame, raytrace_compute.glsl:
- * 277-307); reallocates only if the new scene is larger. Waits for renders
- * queued on the context's own stream; renders on caller streams that read
- * the scene must be complete. */
+ * 277-307); reallocates only if the new scene is larger. Waits (on the host)
+ * for the renders queued that read the scene, on any stream. */
 int rt_scene_update(rt_context *ctx, rt_scene *scene, const rt_object *objs, int n_objs, const rt_material *mats,
                     int n_mats, const rt_light *lights, int n_lights);
 

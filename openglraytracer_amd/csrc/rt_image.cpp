@@ -1,5 +1,7 @@
 // rt_image.cpp — headless image output (the reference displays the texture
 // with a full-screen quad instead: draw_screen_vert/frag.glsl, main.cpp:240-260).
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -9,6 +11,23 @@
 using rtamd::set_error;
 
 extern "C" {
+
+// GL_RGBA8 unorm store of a float colour (main.cpp:152-159, :223): NaN -> 0,
+// clamp to [0, 1], v * 255 rounded to nearest even — the conversion the
+// reference's GL applies (probed: tests/golden/make_rgba8_golden.py); alpha
+// stored as written, 0 (:404).
+int rt_pack_rgba8(const float *in, size_t n_pixels, uint8_t *out) {
+    if ((!in || !out) && n_pixels) {
+        set_error("rt_pack_rgba8: null buffer");
+        return RT_ERR_INVALID;
+    }
+    for (size_t i = 0; i < n_pixels * 4; ++i) {
+        float v = in[i];
+        v = v != v ? 0.0f : std::min(std::max(v, 0.0f), 1.0f);
+        out[i] = static_cast<uint8_t>(std::nearbyint(v * 255.0f));  // default rounding: to nearest even
+    }
+    return RT_OK;
+}
 
 int rt_write_ppm(const char *path, const float *rgba, int width, int height) {
     if (!path || !rgba || width <= 0 || height <= 0) {

@@ -231,6 +231,9 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
                          int width, int height);
 // launch on `stream` with the context's queue slot and kernel-time events
 int launch(rt_context *ctx, LaunchParams &p, int max_depth, hipStream_t stream);
+// a render on `stream` reads `scene`'s blob: remember it (an event on that
+// stream) so that rt_scene_destroy / rt_scene_update wait for it
+int note_scene_use(const rt_scene *scene, hipStream_t stream);
 // bytes per pixel of a surface format (RT_OUTPUT_*)
 inline size_t surface_bytes(int fmt) { return fmt == RT_OUTPUT_RGBA8 ? 4 : (fmt == RT_OUTPUT_RGB32F ? 12 : 16); }
 
@@ -264,4 +267,16 @@ struct rt_scene {
     std::vector<float4> host;    // host copy of the blob (per-frame constants on the host)
     int32_t capacity_units = 0;  // allocated blob size (16-B units)
     rt_context *ctx = nullptr;   // owning context (nullptr once it is destroyed)
+    // Renders that read the blob on streams other than the owning context's:
+    // per stream, an event recorded after its latest such render. The blob
+    // is freed or overwritten only behind all of them (stream order covers
+    // the context's own stream). More than kMaxUseStreams streams: `overflow`,
+    // and the release synchronises the device instead.
+    static constexpr int kMaxUseStreams = 8;
+    struct Use {
+        hipStream_t stream;
+        hipEvent_t done;
+    };
+    mutable std::vector<Use> uses;
+    mutable bool overflow = false;
 };

@@ -43,21 +43,11 @@
 namespace rtamd {
 namespace {
 
-#ifndef RT_WAVES_X
-#define RT_WAVES_X 2
-#endif
-#ifndef RT_WAVES_Y
-#define RT_WAVES_Y 2
-#endif
-#ifndef RT_TILE_ROUNDS
-#define RT_TILE_ROUNDS 1
-#endif
-// A work-group renders a tile of kWavesX x kWavesY wave footprints of 8x8 pixels.
-constexpr int kWavesX = RT_WAVES_X, kWavesY = RT_WAVES_Y;
+// A work-group renders a tile of kWavesX x kWavesY wave footprints of 8x8
+// pixels (2 x 2; 32x8 and 16x32 work-group tiles measured no gain, r01).
+constexpr int kWavesX = 2, kWavesY = 2;
 constexpr int kTileX = 8 * kWavesX, kTileY = 8 * kWavesY;
 constexpr int kThreads = 64 * kWavesX * kWavesY;
-// tiled distribution: a work-group renders kRounds tiles, strided down the frame
-constexpr int kRounds = RT_TILE_ROUNDS;
 
 struct v3 {
     float x, y, z;
@@ -100,14 +90,7 @@ __device__ __forceinline__ Rcp rcp_refined(float b) {
 }
 __device__ __forceinline__ float div_r(float a, Rcp d) {
     const float q = a * d.r;
-#ifdef RT_DIV_TWO  // (the two-correction sequence hipcc's expansion ends with)
-    float t = __builtin_fmaf(-d.b, q, a);
-    const float q1 = __builtin_fmaf(t, d.r, q);
-    t = __builtin_fmaf(-d.b, q1, a);
-    return __builtin_fmaf(t, d.r, q1);
-#else
     return __builtin_fmaf(__builtin_fmaf(-d.b, q, a), d.r, q);
-#endif
 }
 __device__ __forceinline__ float sqrt_short(float x) {
     const float s = __builtin_amdgcn_sqrtf(x);
@@ -118,11 +101,7 @@ __device__ __forceinline__ float sqrt_short(float x) {
 // 1 / sqrt(d), both correctly rounded (GLSL inversesqrt as llvmpipe evaluates
 // it): the refined reciprocal of the short square root
 __device__ __forceinline__ float inv_sqrt(float d) {
-#ifdef RT_DIV_TWO
-    if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return div_r(1.0f, rcp_refined(sqrt_short(d)));
-#else
     if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return rcp_refined(sqrt_short(d)).r;
-#endif
     return 1.0f / sqrtf(d);
 }
 // normalize(v) = v * inversesqrt(dot(v, v))
@@ -137,17 +116,11 @@ __device__ __forceinline__ v3 normalize(v3 a) { return muls(a, inv_sqrt(dot(a, a
 __device__ __forceinline__ bool near_one(float d) { return __float_as_uint(d) - 0x3f7ff800u <= 0x1000u; }
 __device__ __forceinline__ float inv_sqrt_near_one(float d) {
     const uint32_t b = __float_as_uint(d);
-#ifdef RT_BRANCHY
-    const int k = static_cast<int>(b) - 0x3f800000;
-    return __uint_as_float(k >= 0 ? 0x3f800000u - static_cast<uint32_t>(k & ~1)
-                                  : 0x3f800000u + static_cast<uint32_t>((3 - k) >> 2));
-#else
     // both arms computed, then one select (as a ternary the compiler made
     // this a divergent branch)
     const uint32_t above = 0x3f800000u - ((b - 0x3f800000u) & ~1u);  // k >= 0
     const uint32_t below = 0x3f800000u + ((0x3f800003u - b) >> 2);    // k < 0: (3 - k) >> 2
     return __uint_as_float(b >= 0x3f800000u ? above : below);
-#endif
 }
 // normalize() of a vector that is a unit vector up to rounding (a reflected
 // or negated unit vector): the closed form when every lane's squared length
@@ -167,17 +140,12 @@ __device__ __forceinline__ float sphere_sqrt(float qd);
 __device__ __forceinline__ v3 refract(v3 i, v3 n, float eta) {
     const float d = dot(n, i);
     const float k = 1.0f - eta * (eta * (1.0f - d * d));
-#ifdef RT_REFRACT_OLD
-    if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-    return sub(muls(i, eta), muls(n, eta * d + sqrtf(k)));
-#else
     // every lane computes the ray (the short square root when every lane's
     // operand allows it; a total internal reflection lane takes any operand)
     // and total internal reflection selects the zero vector
     const bool tir = k < 0.0f;
     const v3 r = sub(muls(i, eta), muls(n, eta * d + sphere_sqrt(tir ? 1.0f : k)));
     return tir ? mk(0.0f, 0.0f, 0.0f) : r;
-#endif
 }
 // mix(x, y, a) evaluated as x + a * (y - x)
 __device__ __forceinline__ v3 mix(v3 x, v3 y, float a) { return add(x, muls(sub(y, x), a)); }
@@ -225,25 +193,17 @@ __device__ __forceinline__ float glsl_pow(float x, float y) { return glsl_exp2(g
 // vectors is at most about 3 or NaN, so glsl_log2's NaN and +inf cases are
 // never reached; its zero case becomes a select
 __device__ __forceinline__ float glsl_pow_cos(float x, float y) {
-#ifdef RT_POW_FULL
-    return glsl_pow(x, y);
-#else
     const uint32_t i = __float_as_uint(x);
     const float e = static_cast<float>(static_cast<int>((i >> 23) & 0xffu) - 127);
     const float mant = __uint_as_float((i & 0x007fffffu) | 0x3f800000u);
     const float q = div_r(mant - 1.0f, rcp_refined(mant + 1.0f));
-#ifndef RT_POW_SINK
     // computed in every lane (the empty asm pins the value): left to itself
     // the compiler sank the polynomial into a divergent branch around the
     // zero case (configs 3-4 -2 %, config 2 -1 % as a select)
     float lr = __builtin_fmaf(q, poly_log2(q * q), e);
     asm volatile("" : "+v"(lr));
     const float l = x == 0.0f ? -__builtin_inff() : lr;
-#else
-    const float l = x == 0.0f ? -__builtin_inff() : __builtin_fmaf(q, poly_log2(q * q), e);
-#endif
     return glsl_exp2(l * y);
-#endif
 }
 
 // Hardware sqrt (about 1 ulp, no correction steps): culling arithmetic only,
@@ -366,22 +326,12 @@ struct Slab {
     v3 rs, rd, t1, t2;
     float t_near, t_far;
 };
-__device__ __forceinline__ v3 xform_dir(const float *m, v3 d) {
-    // (M * vec4(d, 0)).xyz, GLSL order including the * 0.0 of the w column
-    return mk(m[0] * d.x + m[1] * d.y + m[2] * d.z + m[3] * 0.0f,
-              m[4] * d.x + m[5] * d.y + m[6] * d.z + m[7] * 0.0f,
-              m[8] * d.x + m[9] * d.y + m[10] * d.z + m[11] * 0.0f);
-}
 // (w2l * vec4(d, 0.0)).xyz of a box: the w column's products with 0.0 come
 // precomputed with the record (each is the same float product, +-0 or NaN)
 __device__ __forceinline__ v3 box_dir(const BoxRec &b, v3 d) {
-#ifdef RT_XFORM_MUL0
-    return xform_dir(b.w2l, d);
-#else
     const float *m = b.w2l;
     return mk(m[0] * d.x + m[1] * d.y + m[2] * d.z + b.w2l_w0[0], m[4] * d.x + m[5] * d.y + m[6] * d.z + b.w2l_w0[1],
               m[8] * d.x + m[9] * d.y + m[10] * d.z + b.w2l_w0[2]);
-#endif
 }
 __device__ __forceinline__ v3 xform_point(const float *m, v3 p) {
     return mk(m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3] * 1.0f, m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7] * 1.0f,
@@ -504,7 +454,6 @@ __device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float q
     if (qd < 0.0f) return -1.0f;
     const float sq = sphere_sqrt(qd);
     const float n1 = -qb + sq, n2 = -qb - sq;
-#ifndef RT_TWO_DIV
     if (fminf(fabsf(n1), fabsf(n2)) >= floor) {
         // (the quotient in every lane and a select for t_far < 0 measured
         // slower: config 4 16.57 -> 16.79 ms)
@@ -512,7 +461,6 @@ __device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float q
         inside = n2 < 0.0f;           // t_near < 0
         return (inside ? n1 : n2) / qa2;
     }
-#endif
     const float t1 = n1 / qa2;
     const float t2 = n2 / qa2;
     const float tn = gmin(t1, t2), tf = gmax(t1, t2);
@@ -528,7 +476,6 @@ __device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float q
 __device__ __forceinline__ bool sphere_blocks(float qb, float qc, float qa2, float qa4, float floor) {
     const float qd = qb * qb - qa4 * qc;
     if (!(qd >= 0.0f)) return false;
-#ifndef RT_TWO_DIV
     const float sq = sphere_sqrt(qd);
     const float n1 = -qb + sq, n2 = -qb - sq;
     if (fminf(fabsf(n1), fabsf(n2)) >= floor) {
@@ -536,7 +483,6 @@ __device__ __forceinline__ bool sphere_blocks(float qb, float qc, float qa2, flo
         const float n = n2 < 0.0f ? n1 : n2;
         return n > 0.0f && quotient_below_one(n, qa2);
     }
-#endif
     bool inside;
     const float t = sphere_t(qb, qc, qa2, qa4, __builtin_nanf(""), inside);
     return t > 0.0f && t < 1.0f;
@@ -578,26 +524,6 @@ __device__ __forceinline__ void test_sphere(const Scene &S, int s, v3 start, v3 
 // that margin for origins within 20 units of the centre, so no extra slack
 // is needed: a node whose spheres the exact test could hit before t_limit
 // always passes (tn <= t of the hit < t_limit, tf >= it > 0).
-#ifdef RT_BVH_SLACK
-struct RayInv {
-    v3 o, id;
-};
-__device__ __forceinline__ float safe_rcp(float d) {
-    return fabsf(d) > 1e-30f ? __builtin_amdgcn_rcpf(d) : (__float_as_uint(d) >> 31 ? -1e30f : 1e30f);
-}
-__device__ __forceinline__ RayInv ray_inv(const Ray &r) {
-    return {r.start, mk(safe_rcp(r.dir.x), safe_rcp(r.dir.y), safe_rcp(r.dir.z))};
-}
-__device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, float t_limit) {
-    const float x0 = (lo.x - q.o.x) * q.id.x, x1 = (hi.x - q.o.x) * q.id.x;
-    const float y0 = (lo.y - q.o.y) * q.id.y, y1 = (hi.y - q.o.y) * q.id.y;
-    const float z0 = (lo.z - q.o.z) * q.id.z, z1 = (hi.z - q.o.z) * q.id.z;
-    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-    const float slack = 1e-5f * (fabsf(tn) + fabsf(tf)) + 1e-6f;
-    return tn <= tf + slack && tf >= -slack && tn <= t_limit + 1e-5f * fabsf(t_limit) + slack;
-}
-#else
 struct RayInv {
     v3 oid, id;  // o * id, 1 / d (approximate)
 };
@@ -616,7 +542,6 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
     const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
     return tn <= tf && tf >= 0.0f && tn <= t_limit;
 }
-#endif
 
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
@@ -667,7 +592,6 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         // secondary rays: stackless depth-first BVH walk (skip links)
         const RayInv q = ray_inv(r);
         int node = valid ? 0 : -1;
-#ifndef RT_BVH_INLINE_LEAVES
         // while-while: each lane walks nodes until it holds a leaf (or its
         // walk ends); then the wave tests the spheres of every held leaf
         // together, so the sphere tests of lanes that reach leaves on
@@ -680,17 +604,14 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
         // lane while other lanes look for their first (config 4 18.0 -> 19.0
         // ms, config 3 1.018 -> 1.060 ms).
         int held = 0;  // (count << 24) | first sphere of the held leaf
-#ifndef RT_BVH_FIXED
         // the ray's octant picks its traversal order (nearer child first)
         const int oct = (r.dir.x < 0.0f ? 1 : 0) | (r.dir.y < 0.0f ? 2 : 0) | (r.dir.z < 0.0f ? 4 : 0);
-#endif
         while (__any(node >= 0)) {
             while (node >= 0 && held == 0) {
                 RT_STAT(3, true);
                 RT_STAT(4, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 const float4 lo = S.bvh[2 * node], hi = S.bvh[2 * node + 1];
                 const int leaf = __float_as_int(hi.w);
-#ifndef RT_BVH_FIXED
                 const uint32_t link = S.blink[node * kBvhOctants + oct];
                 if (node_hit(q, lo, hi, h.t)) {
                     held = leaf;
@@ -698,15 +619,6 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
                 } else {
                     node = static_cast<int16_t>(link >> 16);
                 }
-#else
-                const int skip = __float_as_int(lo.w);
-                if (node_hit(q, lo, hi, h.t)) {
-                    held = leaf;
-                    node = leaf ? skip : node + 1;
-                } else {
-                    node = skip;
-                }
-#endif
             }
             if (held) {
                 RT_STAT(5, true);
@@ -715,27 +627,6 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
                 held = 0;
             }
         }
-#else
-        while (node >= 0) {
-            RT_STAT(3, true);
-            RT_STAT(4, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
-            const float4 lo = S.bvh[2 * node], hi = S.bvh[2 * node + 1];
-            const int leaf = __float_as_int(hi.w);
-            if (node_hit(q, lo, hi, h.t)) {
-                if (leaf) {
-                    const int first = leaf & 0xFFFFFF, count = leaf >> 24;
-                    RT_STAT(5, true);
-                    for (int s = first; s < first + count; ++s)
-                        test_sphere(S, s, r.start, d2, qa2, qa4, floor, false, h);
-                    node = __float_as_int(lo.w);
-                } else {
-                    node = node + 1;
-                }
-            } else {
-                node = __float_as_int(lo.w);
-            }
-        }
-#endif
     } else {
         for (int s = 0; s < S.ns; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, floor, kPrimary, h);
     }
@@ -788,20 +679,12 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     RT_STAT(7, need);
     RT_STAT(10, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
     for (int b = 0; b < S.nb; ++b) {
-#ifdef RT_BOX_GUARD
-        if (need && !hit) hit = box_occludes(cload(S.cbox + b), start, dir, light_bit);
-#else
         // every lane tests (no divergent branch around the test; lanes
         // without the query or already shadowed keep their flag)
         const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit);
         hit = hit | (need & occ);
-#endif
     }
     if (!__any(need && !hit)) return hit;
-#ifdef RT_ABLATE_SPHSHADOW
-    return hit;
-#endif
-#ifndef RT_SHADOW_EAGER_TERMS
     if (S.cull && !S.gmask && S.dmask) {
         // the LDS-mask walk (see below) with the ray's quadratic terms
         // computed only when some lane of the wave has a candidate (most
@@ -838,15 +721,11 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
         }
         return hit;
     }
-#endif
     const v3 d2 = muls(dir, 2.0f);
     const float qa = dot(dir, dir);
     const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
     const float floor = root_floor(qa2);
     auto exact = [&](int s) {
-#ifdef RT_ABLATE_EXACT
-        if (s < 0)
-#endif
         if (need && !hit) {
             RT_STAT(8, true);
             const float4 c = S.sph[s];
@@ -859,16 +738,12 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     // the same test for the mask walks, whose candidate words are already
     // empty for lanes without the query or with a hit
     auto exact_cand = [&](int s) {
-#ifdef RT_EXACT_GUARD
-        exact(s);
-#else
         RT_STAT(8, true);
         const float4 c = S.sph[s];
         const v3 oc = sub(start, mk(c.x, c.y, c.z));
         const float qb = dot(d2, oc);
         const float qc = dot(oc, oc) - c.w;
         hit = sphere_blocks(qb, qc, qa2, qa4, floor);
-#endif
     };
     if (!S.cull) {
         for (int s = 0; s < S.ns; ++s) {
@@ -1093,7 +968,7 @@ __device__ unsigned long long rt_phase_buf[kPhaseWaves * 16];
 // the clock read after `v` is available (a branch on it orders the read)
 #define RT_PHASE_AFTER(k, v)                     \
     do {                                         \
-        if ((v) != -123456789) RT_PHASE(k);      \
+        if ((v) != -12345) RT_PHASE(k);      \
     } while (0)
 #else
 #define RT_PHASE_AFTER(k, v) \
@@ -1118,9 +993,6 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
         const v3 ldir = normalize(sdir);
         const float cos_theta = dot(ldir, c.n);
-#ifdef RT_REFLECT_DOT
-        const v3 lref = normalize_unit(reflect(muls(ldir, -1.0f), c.n));
-#else
         // reflect(-ldir, n) needs dot(n, -ldir), which is -cos_theta (exact
         // negation, commuted products) except that an exactly-zero dot may
         // differ in the sign of its zero; that only flips signs of zero
@@ -1128,26 +1000,17 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         // zero, and max(cos_phi, 0) is +0 for both: the result is identical
         const v3 nl = muls(ldir, -1.0f);
         const v3 lref = normalize_unit(sub(nl, muls(c.n, 2.0f * -cos_theta)));
-#endif
         const float cos_phi = dot(view, lref);
         const LightMatRec &q = S.lm[c.material * S.nl + j];
         const float kd = gmax(cos_theta, 0.0f);
         // pow(0, s) is +0 for s > 0 (log2 = -inf, exp2 clamps to 2^-127
         // scaled to 0): skip the polynomials when no lane needs them
         const float xs = gmax(cos_phi, 0.0f);
-#ifdef RT_BRANCHY
-        const bool need_pow = !(xs == 0.0f && m.shininess > 0.0f);
-#else
         // flags combined with & and |, not && and ||: short-circuit evaluation
         // of LDS-loaded operands compiled to nested divergent branches
         const bool need_pow = !((xs == 0.0f) & (m.shininess > 0.0f));
-#endif
         float ks = 0.0f;
-#ifdef RT_ABLATE_POW
-        ks = xs;
-#else
         if (__any(need_pow && valid)) ks = need_pow ? glsl_pow_cos(xs, m.shininess) : 0.0f;
-#endif
         const float4 nd = make_float4(dif.x + q.ld_md[0] * kd, dif.y + q.ld_md[1] * kd, dif.z + q.ld_md[2] * kd,
                                       dif.w + q.ld_md[3] * kd);
         const float4 ns = make_float4(spe.x + q.ls_ms[0] * ks, spe.y + q.ls_ms[1] * ks, spe.z + q.ls_ms[2] * ks,
@@ -1155,11 +1018,7 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
         // the shadow ray matters only if the light's term can change the sums
         // (host flags, rt_scene.cpp: with a tame material a zero factor or a
         // zero product adds +-0 to sums that are never -0)
-#ifdef RT_BRANCHY
-        const bool changes = q.always || (kd != 0.0f && q.d_nz) || (ks != 0.0f && q.s_nz);
-#else
         const bool changes = (q.always != 0) | ((kd != 0.0f) & (q.d_nz != 0)) | ((ks != 0.0f) & (q.s_nz != 0));
-#endif
         const bool need = valid && changes;
         if (j == 1) RT_PHASE(5);
 #ifdef RT_ABLATE_SHADOW
@@ -1306,12 +1165,7 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
             Frame fr;
             fr.col = col;
             fr.rs = sub(c.p, muls(c.n, 0.001f));
-#ifdef RT_IOR_DIV
-            float ratio = 1.0f / m.refraction_index;
-            if (c.inside) ratio = 1.0f / ratio;
-#else
             const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
-#endif
             fr.rd = refract(ray.dir, c.n, ratio);
             fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3);
             F.set(level, fr);
@@ -1355,140 +1209,6 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
         }
     }
     return result;
-}
-
-// Wave-uniform tree walk (RT_TRACE_TREE=trace_tree_u; measured slower, see
-// below). All 64 lanes of a wave visit the nodes
-// of the full binary ray tree (reflection child first, then refraction
-// child, as the stack machine does, :979-1030) in the same depth-first order;
-// a node is visited when some lane's own tree contains it, and the lanes
-// whose tree does not ride along inactive (`on` = false). The level is
-// therefore wave-uniform, so each level's frame is a fixed set of registers
-// (selected by a scalar level, no scratch), and the rays a wave traces
-// together are the same kind of ray (primary, reflected at level 1, ...) —
-// more coherent than rays of different tree positions. Per level and lane a
-// frame holds the node's colour (phong, then mixed with the reflection), the
-// pending refraction ray and (material | on | sr | st); whether the level is
-// in its refraction child is one uniform bit.
-struct UFrame {
-    v3 col, rs, rd;
-    int mf;  // material | kOn | kSr | kSt
-};
-constexpr int kOn = 1 << 16, kSr = 1 << 17, kSt = 1 << 18;
-
-__device__ __forceinline__ UFrame pick(bool c, const UFrame &a, const UFrame &b) {
-    UFrame r;
-    r.col = sel(c, a.col, b.col);
-    r.rs = sel(c, a.rs, b.rs);
-    r.rd = sel(c, a.rd, b.rd);
-    r.mf = c ? a.mf : b.mf;
-    return r;
-}
-
-// One frame per level as distinct members (no array: nothing for the
-// compiler to index dynamically, so the frames stay in registers).
-template <int N>
-struct UStack {
-    UFrame head;           // level 0 of this sub-stack
-    UStack<N - 1> tail;    // levels 1..N-1
-    // `level` is wave-uniform: every lane takes the same arm
-    __device__ __forceinline__ UFrame get(int level) const {
-        // value selects field by field (a select between the members'
-        // addresses would pin the frames in memory)
-        return pick(level == 0, head, tail.get(level - 1));
-    }
-    __device__ __forceinline__ void set(int level, const UFrame &v) {
-        head = pick(level == 0, v, head);
-        tail.set(level - 1, v);
-    }
-};
-template <>
-struct UStack<1> {
-    UFrame head;
-    __device__ __forceinline__ UFrame get(int) const { return head; }
-    __device__ __forceinline__ void set(int, const UFrame &v) { head = v; }
-};
-
-template <int kDepth>
-__device__ __forceinline__ v3 trace_tree_u(const Scene &S, Ray ray, bool active) {
-    const v3 black = mk(0.0f, 0.0f, 0.0f);
-    UStack<kDepth> F;
-    uint32_t refr_phase = 0u;  // bit P: level P is in its refraction child (uniform)
-    int level = 0;             // uniform
-    bool on = active;
-    v3 value = black;
-    for (;;) {
-        RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
-        const Hit h = level == 0 ? closest<true>(S, ray, on) : closest<false>(S, ray, on);
-        const bool hit = on && h.obj >= 0;
-        Collision c;
-        c.material = 0;
-        v3 col = black;
-        if (__any(hit)) {
-            c = level == 0 ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
-#ifdef RT_ABLATE_PHONG
-            col = add(c.p, c.n);
-#else
-            col = phong(S, ray, c, hit);
-#endif
-        }
-        value = hit ? col : black;  // a missed ray is black (:962-963)
-        if (level < kDepth) {
-            const MatRec &m = S.mat[c.material];
-            const bool sr = hit && m.reflectivity > 0.0f;   // :979-997
-            const bool st = hit && m.transparency > 0.0f;   // :1001-1030
-            const bool any_sr = __any(sr);
-            if (any_sr || __any(st)) {  // push this node, descend into its first child
-                UFrame fr;
-                fr.col = value;
-                fr.rs = sub(c.p, muls(c.n, 0.001f));
-                const float ratio = c.inside ? m.eta_out : m.eta_in;
-                fr.rd = refract(ray.dir, c.n, ratio);
-                fr.mf = c.material | (on ? kOn : 0) | (sr ? kSr : 0) | (st ? kSt : 0);
-                F.set(level, fr);
-                if (any_sr) {
-                    ray.start = add(c.p, muls(c.n, 0.001f));
-                    ray.dir = reflect(ray.dir, c.n);
-                    on = sr;
-                    refr_phase &= ~(1u << level);
-                } else {
-                    ray.start = fr.rs;
-                    ray.dir = fr.rd;
-                    on = st;
-                    refr_phase |= 1u << level;
-                }
-                ++level;
-                continue;
-            }
-        }
-        // this node is finished: fold the finished subtrees into their parents
-        bool next_child = false;
-        while (level > 0) {
-            const int P = level - 1;
-            UFrame fr = F.get(P);
-            const MatRec &m = S.mat[fr.mf & 0xFFFF];
-            const bool f_sr = fr.mf & kSr, f_st = fr.mf & kSt;
-            if (!((refr_phase >> P) & 1u)) {  // back from the reflection child
-                if (f_sr) fr.col = mix(fr.col, value, m.reflectivity);
-                if (__any(f_st)) {  // the refraction child comes next
-                    F.set(P, fr);
-                    refr_phase |= 1u << P;
-                    ray.start = fr.rs;
-                    ray.dir = fr.rd;
-                    on = f_st;
-                    next_child = true;
-                    break;
-                }
-                value = fr.col;
-            } else {  // back from the refraction child
-                value = f_st ? mix(fr.col, value, m.transparency) : fr.col;
-            }
-            on = (fr.mf & kOn) != 0;
-            --level;
-        }
-        if (!next_child) break;
-    }
-    return value;
 }
 
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
@@ -1536,15 +1256,6 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
     return static_cast<float>(h >> 8) * (1.0f / 16777216.0f);
 }
 
-// The per-lane walk (trace_tree) is the default: at 6 waves per SIMD it
-// measured faster than the wave-uniform walk (trace_tree_u), whose frames
-// stay in registers only above 120 VGPRs (config 4, 7680x4320 depth 4:
-// per-lane 25.0 ms; uniform 32.5 / 25.9 / 27.2 / 33.3 ms at 6 / 5 / 4 / 3
-// waves per SIMD; config 3: 1.139 vs 1.114 / 1.153 / 1.289 / 1.282 ms;
-// frames bit-identical; profiles/r02b_tree_walk_ab.log).
-#ifndef RT_TRACE_TREE
-#define RT_TRACE_TREE trace_tree
-#endif
 
 // Occupancy target per depth: the recursive kernels (depth >= 2) keep the
 // tree walk's frames in scratch either way and hide its latency best at 6
@@ -1586,9 +1297,6 @@ __device__ __forceinline__ void frame_setup(const LaunchParams &p, const FrameVi
     const int hw = p.width / 2, hh = p.height / 2;
     const bool cull = V.cull && hw > 0 && hh > 0;
     const float *P = V.proj;
-#ifdef RT_ABLATE_SETUP
-    if (p.n_spheres >= 0) return;
-#endif
     for (int item = threadIdx.x; item < 8 * p.n_spheres; item += kThreads) {  // whole groups of 8 lanes
         const int s = item >> 3, i = item & 7;
         const float4 c = blob[p.off_spheres + s];
@@ -1701,13 +1409,14 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
     if constexpr (!kAccum) {
         const Ray ray = have_pre ? pre : camera_ray(p, V, x, y, 0.0f, 0.0f);
 #if defined(RT_ABLATE_RAYGEN)
+        (void)ray;
         const v3 col = mk(float(x), float(y), 0.0f);
 #elif defined(RT_ABLATE_TRACE)
         const v3 col = ray.dir;
 #else
         v3 col;
         if constexpr (kDepth == 0) col = trace0(S, ray, active);
-        else col = RT_TRACE_TREE<kDepth>(S, ray, active);
+        else col = trace_tree<kDepth>(S, ray, active);
 #endif
         if (active) store_pixel(p, z, idx, col);
     } else {
@@ -1719,7 +1428,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
             const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
             v3 col;
             if constexpr (kDepth == 0) col = trace0(S, camera_ray(p, V, x, y, jx, jy), active);
-            else col = RT_TRACE_TREE<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active);
+            else col = trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active);
             acc = add(acc, col);
         }
         if (active) {
@@ -1749,10 +1458,9 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 // Queued distribution pays where the cost per wave tile varies most (the
 // recursive depths); depth 0 / 1 keep the tiled kernel, whose body the
 // compiler schedules with fewer registers (config 2: 70 vs 81 VGPRs).
-#ifndef RT_QUEUED_MIN_DEPTH  // r02: queued from depth 0 (64 VGPRs + 84 B scratch): config 2 single frame
-#define RT_QUEUED_MIN_DEPTH 2  // 52 -> 67 us, 8-frame launches (tiled either way) 41.5 -> 50.6 us per frame
-#endif
-constexpr bool kQueuedDepth(int depth) { return depth >= RT_QUEUED_MIN_DEPTH; }
+// (r02: queued from depth 0, 64 VGPRs + 84 B scratch: config 2 single frame
+// 52 -> 67 us, 8-frame launches, tiled either way, 41.5 -> 50.6 us per frame)
+constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 
 template <int kDepth, bool kAccum>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
@@ -1829,10 +1537,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.dmask_bytes = p.dmask_bytes;
     // (recursive depths only: the depth-0/1 kernels keep their register
     // budget and use the per-wave cone for such scenes)
-#ifndef RT_GMASK_MINDEPTH
-#define RT_GMASK_MINDEPTH 2
-#endif
-    S.gmask = kDepth >= RT_GMASK_MINDEPTH && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
+    S.gmask = kDepth >= 2 && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
     S.gwords = p.gmask_words;
     S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
     S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
@@ -1854,21 +1559,6 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // queue's head (one render call site for both: the kernel body is inlined once)
     int t = queued ? g : 0;
     RT_PHASE(1);
-#if RT_TILE_ROUNDS > 1
-    if (!queued) {
-        const int stride_y = static_cast<int>(gridDim.y) * kWavesY;
-        if constexpr (!kAccum)
-            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, own_ray, true);
-        else
-            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, own_wy, z, own, own_ray, false);
-        for (int r = 1; r < kRounds; ++r) {
-            const int wy = own_wy + r * stride_y;
-            if (wy * 8 >= p.n_rows) break;
-            render_wave_tile<kDepth, kAccum>(p, S, V, own_wx, wy, z, wave_pixel(p, own_wx, wy), own_ray, false);
-        }
-        return;
-    }
-#endif
     while (t < total) {
         int nxt = 0;
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
@@ -1914,7 +1604,7 @@ template <int kDepth, bool kAccum>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
     const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
-    dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY * kRounds - 1) / (kTileY * kRounds), p.n_views);
+    dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY - 1) / kTileY, p.n_views);
     const int wave_tiles = ((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
     // queued: more wave tiles than resident waves, and every queue has a

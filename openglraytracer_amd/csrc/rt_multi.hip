@@ -233,6 +233,7 @@ int rt_render_multi_view(rt_multi *m, const rt_scene *const *scenes, const rt_vi
             p.shard = i;
             p.out = static_cast<float4 *>(dst);
             if ((rc = launch(c, p, max_depth, c->stream)) != RT_OK) return rc;
+            if ((rc = note_scene_use(scenes[i], c->stream)) != RT_OK) return rc;
         }
         if ((e = hipEventRecord(m->rendered[i], c->stream)) != hipSuccess) return hip_fail("hipEventRecord", e);
     }

@@ -30,9 +30,29 @@ def run_bench(n, *args, timeout=240):
 
 
 @pytest.mark.gpu
+def test_config2_two_ranks_row_tiled_gather():
+    """The default config2 shape at N>1 (north_star): every frame row-tiled
+    over the ranks, the GL_RGBA8 shards gathered to rank 0 and
+    de-interleaved there; the assembled frames equal rank 0's whole-frame
+    render byte for byte (bench.py checks, `verified`), through the HIP
+    kernel."""
+    line = run_bench(2, "--steps", "3", "--warmup", "1", "--frames", "3")
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
+    assert line["config"]["frames_per_step"] == 3 and "gather" in line["timing"]["collective"]
+    assert "GL_RGBA8" in line["config"]["output"]
+    ranks = line["timing"]["per_rank"]
+    assert [r["rank"] for r in ranks] == [0, 1] and all(r["kernel_ms"] > 0 and r["collective_ms"] > 0 for r in ranks)
+    assert line["roofline"]["bytes_per_launch"] == 3 * 1920 * 540 * 4  # 4 B per pixel, half the rows
+    v = line["verified"]
+    assert v["bit_exact"] and v["frames_checked"] == 3 and v["mismatched_pixels"] == 0
+    ind = line["independent_frames"]
+    assert ind["frames_per_step"] == 6 and ind["scaling"] == "weak" and ind["value"] > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["none", "all_to_all"])
-def test_config2_two_ranks(mode):
-    line = run_bench(2, "--steps", "3", "--warmup", "1", "--frames-per-gpu", "2", "--frame-exchange", mode)
+def test_config2_two_ranks_other_modes(mode):
+    line = run_bench(2, "--steps", "3", "--warmup", "1", "--frames", "2", "--frame-exchange", mode)
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["value"] > 0
     assert line["config"]["frames_per_step"] == 4
     ranks = line["timing"]["per_rank"]
@@ -40,9 +60,11 @@ def test_config2_two_ranks(mode):
     if mode == "none":
         assert line["timing"]["collective"] == "none" and "no collective" in line["config"]["parallelism"]
         assert line["roofline"]["bytes_per_launch"] == 2 * 1920 * 1080 * 16
+        assert "verified" not in line
     else:
         assert "all_to_all" in line["timing"]["collective"]
         assert all(r["collective_ms"] > 0 for r in ranks)
+        assert line["verified"]["bit_exact"] and line["verified"]["frames_checked"] == 4
 
 
 @pytest.mark.gpu
@@ -52,9 +74,33 @@ def test_config3_two_ranks_gather():
     assert all(r["collective_ms"] > 0 and r["kernel_ms"] > 0 for r in line["timing"]["per_rank"])
     # each rank stores its float3 row blocks: half the frame's rows each
     assert line["roofline"]["bytes_per_launch"] == 3840 * 1080 * 12
+    assert line["verified"]["bit_exact"] and line["verified"]["frames_checked"] == 1
 
 
 @pytest.mark.gpu
 def test_config5_two_ranks_all_reduce():
     line = run_bench(2, "--workload", "config5", "--steps", "2", "--warmup", "1")
     assert "all_reduce" in line["timing"]["collective"] and line["value"] > 0
+
+
+def test_pmc_summary_of_other_sources_is_not_reported(tmp_path, monkeypatch):
+    """bench.py reads the committed PMC summary only when it was profiled on
+    the same sources (the src hash of rt_version()); otherwise the line says
+    which build the summary belongs to instead of mixing builds."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    summary = {"workload": "config4", "n_gpus": 1, "frames_per_launch": 1, "sq_insts_valu_per_launch": 1e9,
+               "hbm_bytes_per_launch": 5e9,
+               "build": "openglraytracer_amd 0.3 (gfx950, src 0123456789ab, git abc-dirty)"}
+    (prof / "pmc_config4_latest.json").write_text(json.dumps(summary))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    same = bench.pmc_latest("config4", 1, "openglraytracer_amd 0.3 (gfx950, src 0123456789ab, git def)")
+    assert same["hbm_bytes_per_launch"] == 5e9 and bench.valu_bound(same, 10.0)["wave_insts_per_launch"] == 1e9
+    other = bench.pmc_latest("config4", 1, "openglraytracer_amd 0.3 (gfx950, src fedcba987654, git abc)")
+    assert "hbm_bytes_per_launch" not in other and other["stale_build"] == summary["build"]
+    assert "stale_build" in bench.valu_bound(other, 10.0)
+    assert bench.pmc_latest("config3", 1, summary["build"]) == {}

@@ -66,7 +66,7 @@ def exchange_worker(rank, world, port, result_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     objs = scenes.bench_objects(16)
-    fpr = 2  # frames per rank in flight (bench.py --frames-per-gpu)
+    fpr = 2  # frames per rank in flight (bench.py --frames with --frame-exchange all_to_all)
     times = [k / 60.0 for k in range(world * fpr)]
     ids = frame.shard_row_ids(H, BLOCK, world, rank)
     # the batch buffer rt_render_batch writes in bench.py's exchange format
@@ -158,4 +158,42 @@ def test_row_tiled_frame_gathers_to_rank0(tmp_path, world):
     out = str(tmp_path / "frame.npy")
     mp.start_processes(gather_frame_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
     full = oracle_port.render(scenes.bench_objects(64), W, H, 2, 0.0)[..., :3]
+    assert np.array_equal(np.load(out), full)
+
+
+def rgba8_gather_worker(rank, world, port, result_path):
+    """bench.py config2 at N ranks (the default --frame-exchange gather): F
+    frames row-tiled in interleaved blocks, each rank's blocks of all F
+    frames in the GL_RGBA8 surface format (RT_OUTPUT_RGBA8: one 4-byte texel
+    per pixel, moved as int32), one gather to rank 0, de-interleaved there."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import openglraytracer_amd as rt
+    from openglraytracer_amd import frame
+    from oracle import port as oracle_port, scenes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    objs = scenes.bench_objects(16)
+    ids = frame.shard_row_ids(H, BLOCK, world, rank)
+    buf = torch.zeros(frame.flat_shard_elems(FRAMES, H, W, BLOCK, world, channels=1), dtype=torch.int32)
+    data = np.stack([rt.pack_rgba8(np.concatenate([oracle_port.render(objs, W, H, DEPTH, t, rows=(int(r), int(r) + 1))
+                                                   for r in ids])) for t in TIMES])
+    texels = np.ascontiguousarray(data).view(np.int32)  # (F, rows, W, 1)
+    buf[: texels.size] = torch.from_numpy(texels.reshape(-1))
+    gathered = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gathered, dst=0)
+    if rank == 0:
+        out = frame.assemble(gathered, FRAMES, H, W, BLOCK, channels=1).numpy()
+        np.save(result_path, np.ascontiguousarray(out).view(np.uint8).reshape(FRAMES, H, W, 4))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rgba8_frames_gather_to_rank0(tmp_path, world):
+    import openglraytracer_amd as rt
+    from oracle import port as oracle_port, scenes
+    out = str(tmp_path / "frames.npy")
+    mp.start_processes(rgba8_gather_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
+    full = np.stack([rt.pack_rgba8(oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, t)) for t in TIMES])
     assert np.array_equal(np.load(out), full)

@@ -107,8 +107,9 @@ def test_config2_full_frame_bit_exact(gpu_ctx):
     assert np.array_equal(g, o), parity_stats(g, o)
 
 
-@pytest.mark.parametrize("cfg,band", [("config3", [(0, 8), (1076, 1084), (2152, 2160)]),
-                                      ("config4", [(2156, 2164)])])
+@pytest.mark.parametrize("cfg,band", [("config3", [(0, 8), (536, 544), (1076, 1084), (1620, 1628), (2152, 2160)]),
+                                      ("config4", [(2156, 2164), (0, 8), (1080, 1088), (3240, 3248),
+                                                   (4312, 4320)])])
 def test_large_configs_bands_bit_exact(gpu_ctx, cfg, band):
     build, w, h, depth = scenes.CONFIGS[cfg]
     objs = build()
@@ -721,12 +722,16 @@ def test_multi_gpu_group_equals_single_frame(fmt, block):
             c.close()
 
 
-def test_multi_gpu_group_rccl():
+def test_multi_gpu_group_rccl_transport():
     """The RCCL transport (ncclCommInitAll over the contexts' devices, grouped
-    ncclSend / ncclRecv to the root): on every GPU of the box, one context
-    each; bit-identical to the single-GPU frame. Two contexts on one device
-    are refused (RCCL needs distinct devices)."""
+    ncclSend / ncclRecv to the root, rt_multi.hip): one context on every GPU
+    of the box; bit-identical to the single-GPU frame, and the gather moved
+    the shards (its time is measured). Needs two devices: on a one-GPU box
+    the send / receive loop would not run, so the test is skipped there
+    rather than reported as covering it."""
     n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("the RCCL transport needs at least 2 GPUs (this box has %d)" % n)
     objs = scenes.bench_objects(64)
     w, h, depth = 640, 360, 2
     view = rt.make_view(None, 0.0)
@@ -738,17 +743,70 @@ def test_multi_gpu_group_rccl():
         try:
             for block in (8, 16):
                 assert np.array_equal(group.render(scs, w, h, depth, view=view, block_rows=block), whole)
+                kms, gather_ms, _ = group.last_ms()
+                assert gather_ms > 0.0 and all(k > 0.0 for k in kms[:n])
         finally:
             group.close()
-        extra = rt.Context(0)
-        try:
-            with pytest.raises(rt.RTError) as e:
-                rt.Multi([ctxs[0], extra], transport=rt.abi.RT_MULTI_RCCL)
-            assert e.value.code == rt.abi.RT_ERR_INVALID
-        finally:
-            extra.close()
     finally:
         for s in scs:
             s.close()
         for c in ctxs:
             c.close()
+
+
+def test_multi_gpu_group_rccl_refuses_shared_device():
+    """RCCL needs distinct devices: two contexts on one device are refused
+    (the COPY transport serves them, test_multi_gpu_group_equals_single_frame)."""
+    a, b = rt.Context(0), rt.Context(0)
+    try:
+        with pytest.raises(rt.RTError) as e:
+            rt.Multi([a, b], transport=rt.abi.RT_MULTI_RCCL)
+        assert e.value.code == rt.abi.RT_ERR_INVALID
+    finally:
+        a.close()
+        b.close()
+
+
+def test_scene_destroy_right_after_async_render_on_a_torch_stream(gpu_ctx):
+    """rt_scene_destroy frees the blob in stream order on the context's
+    stream behind the renders of it on other streams (an event per stream,
+    rt_api.cpp note_scene_use): destroying a scene right after an
+    asynchronous render on a torch stream, then creating a new scene (which
+    may reuse the memory) and rendering it, leaves both frames intact."""
+    objs_a, objs_b = scenes.bench_objects(64), scenes.bench_objects(64, 7)
+    w, h, depth = 1920, 1080, 2
+    view = rt.make_view(None, 0.0)
+    want_a = gpu_render(gpu_ctx, objs_a, w, h, depth, view)
+    want_b = gpu_render(gpu_ctx, objs_b, w, h, depth, view)
+    s = torch.cuda.Stream()
+    for _ in range(3):
+        out_a = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+        out_b = torch.empty_like(out_a)
+        sa = rt.Scene(gpu_ctx, objs_a)
+        rt.render_device(gpu_ctx, sa, out_a.data_ptr(), w, h, depth, view=view, stream=s.cuda_stream)
+        sa.close()  # the render above may still be running on `s`
+        sb = rt.Scene(gpu_ctx, objs_b)
+        rt.render_device(gpu_ctx, sb, out_b.data_ptr(), w, h, depth, view=view, stream=s.cuda_stream)
+        s.synchronize()
+        sb.close()
+        assert np.array_equal(out_a.cpu().numpy(), want_a)
+        assert np.array_equal(out_b.cpu().numpy(), want_b)
+
+
+def test_scene_update_waits_for_renders_on_other_streams(gpu_ctx):
+    """rt_scene_update overwrites the blob only after the renders of it on
+    any stream have finished."""
+    objs_a, objs_b = scenes.bench_objects(64), scenes.bench_objects(64, 7)
+    w, h, depth = 1920, 1080, 2
+    view = rt.make_view(None, 0.0)
+    want_a = gpu_render(gpu_ctx, objs_a, w, h, depth, view)
+    s = torch.cuda.Stream()
+    sc = rt.Scene(gpu_ctx, objs_a)
+    try:
+        out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_device(gpu_ctx, sc, out.data_ptr(), w, h, depth, view=view, stream=s.cuda_stream)
+        sc.update(objs_b)
+        s.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want_a)
+    finally:
+        sc.close()

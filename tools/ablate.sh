@@ -24,6 +24,6 @@ if [ "${1:-}" = flags ]; then
   exit 0
 fi
 for v in full:"" noshadow:"-DRT_ABLATE_SHADOW" nophong:"-DRT_ABLATE_PHONG" notrace:"-DRT_ABLATE_TRACE" \
-         nostage:"-DRT_ABLATE_TRACE -DRT_ABLATE_STAGE" noraygen:"-DRT_ABLATE_TRACE -DRT_ABLATE_STAGE -DRT_ABLATE_RAYGEN"; do
+         noraygen:"-DRT_ABLATE_RAYGEN" noframes:"-DRT_ABLATE_FRAMES"; do
   build ${v%%:*} openglraytracer_amd/csrc "${v#*:}"
 done

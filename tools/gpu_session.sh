@@ -31,4 +31,10 @@ fi
 if want prof2; then
   step prof_config2 900 tools/profile.sh $tag/c2 --steps 50 --warmup 5
 fi
+if want prof5; then
+  step prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
+fi
+if want ab; then  # tools/ab.py over the builds under _ab/ (tools/ablate.sh)
+  step ab 900 python tools/ab.py ${AB_ARGS:-}
+fi
 echo done
