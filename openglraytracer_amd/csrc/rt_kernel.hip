@@ -258,6 +258,44 @@ __shared__ unsigned rt_stats_lds[16][kStats];
     } while (0)
 #endif
 
+// Development probe (RT_CYCLES builds only, tools/cycles.py): wave time per
+// phase. At every phase switch the first active lane of the wave adds the
+// shader-clock cycles since the previous switch to the phase being left
+// (per-wave slots in LDS, flushed once per wave), so the sums are wave-time
+// — issue and stalls alike — attributed to where the wave was.
+enum CycPhase {
+    kCycPrologue, kCycRaygen, kCycClosest1, kCycClosest2, kCycResolve, kCycPhong, kCycShadow, kCycWalk,
+    kCycStore, kCycPhases
+};
+#ifdef RT_CYCLES
+__device__ unsigned long long rt_cycles[16];
+__shared__ unsigned long long rt_cyc_lds[16][kCycPhases + 1];  // [wave][phase], [kCycPhases]: last switch
+__shared__ int rt_cyc_cur[16];
+#define RT_CYC(next)                                                                     \
+    do {                                                                                 \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();                    \
+        const int w_ = threadIdx.x >> 6;                                                 \
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {                         \
+            rt_cyc_lds[w_][rt_cyc_cur[w_]] += now_ - rt_cyc_lds[w_][kCycPhases];         \
+            rt_cyc_lds[w_][kCycPhases] = now_;                                           \
+            rt_cyc_cur[w_] = (next);                                                     \
+        }                                                                                \
+    } while (0)
+// the switch after `v` is computed
+#define RT_CYC_AFTER(next, v)                   \
+    do {                                        \
+        asm volatile("" ::"v"(v));              \
+        RT_CYC(next);                           \
+    } while (0)
+#else
+#define RT_CYC(next) \
+    do {             \
+    } while (0)
+#define RT_CYC_AFTER(next, v) \
+    do {                      \
+    } while (0)
+#endif
+
 // A record read through the constant address space, dword by dword (scalar
 // loads when the address is wave-uniform).
 template <class T>
@@ -545,7 +583,7 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
 
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
+__device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool valid) {
     Hit h{10000.0f, -1, 0, 0};
     RT_STAT(kPrimary ? 0 : 1, valid);
     RT_STAT(kPrimary ? 13 : 2, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
@@ -633,6 +671,13 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid)
     if (!valid) h.obj = -1;
     return h;
 }
+template <bool kPrimary>
+__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
+    RT_CYC(kPrimary ? kCycClosest1 : kCycClosest2);
+    const Hit h = closest_impl<kPrimary>(S, r, valid);
+    RT_CYC_AFTER(kCycWalk, h.t);
+    return h;
+}
 
 // Mask of the texel of direction u in a light's cube map (rt_internal.h,
 // kMaskMaxSpheres): face = the largest |component| (ties to the lower axis),
@@ -672,8 +717,8 @@ __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int b
 // first pass over the LDS mask that drops such candidates before the exact
 // walk (config 2 even).
 // p = the shaded point, L = the light. Called with all lanes active.
-__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
-                                         uint64_t mask, bool need) {
+__device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
+                                              uint64_t mask, bool need) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     RT_STAT(7, need);
@@ -904,6 +949,14 @@ __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p,
     return hit;
 }
 
+__device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
+                                         uint64_t mask, bool need) {
+    RT_CYC(kCycShadow);
+    const bool hit = occluded_impl(S, start, dir, p, L, light, slot, mask, need);
+    RT_CYC_AFTER(kCycPhong, hit ? 1 : 0);
+    return hit;
+}
+
 struct Collision {
     v3 p, n;
     bool inside;
@@ -914,7 +967,7 @@ struct Collision {
 // A box's slab distances come with the hit (the closest-hit loop computed
 // them); its t is the slab test's intersection distance.
 template <bool kPrimary>
-__device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const Hit &h, bool valid) {
+__device__ __forceinline__ Collision resolve_impl(const Scene &S, const Ray &r, const Hit &h, bool valid) {
     Collision c;
     c.p = mk(0.0f, 0.0f, 0.0f);
     c.n = mk(0.0f, 0.0f, 1.0f);
@@ -952,6 +1005,13 @@ __device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const
     }
     return c;
 }
+template <bool kPrimary>
+__device__ __forceinline__ Collision resolve(const Scene &S, const Ray &r, const Hit &h, bool valid) {
+    RT_CYC(kCycResolve);
+    const Collision c = resolve_impl<kPrimary>(S, r, h, valid);
+    RT_CYC_AFTER(kCycWalk, c.p.x);
+    return c;
+}
 
 // Development probe (timing builds only, tools/phase_trace.py): lane 0 of
 // every wave of a depth-0 tiled launch records the 100 MHz real-time clock
@@ -980,7 +1040,7 @@ __device__ unsigned long long rt_phase_buf[kPhaseWaves * 16];
 #endif
 
 // ads_phong_lighting (:789-840). Called with all lanes active.
-__device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collision &c, bool valid) {
+__device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Collision &c, bool valid) {
     const MatRec &m = S.mat[c.material];
     float4 dif = make_float4(0.0f, 0.0f, 0.0f, 0.0f), spe = dif;
     const v3 view = normalize_unit(muls(r.dir, -1.0f));  // ray directions are unit vectors up to rounding
@@ -1054,6 +1114,12 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
     const float pz = ((m.amb_sum[2] + dif.z) + spe.z) + m.emissive[2];
     const float pw = ((m.amb_sum[3] + dif.w) + spe.w) + m.emissive[3];
     return mk(px * pw, py * pw, pz * pw);
+}
+__device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collision &c, bool valid) {
+    RT_CYC(kCycPhong);
+    const v3 col = phong_impl(S, r, c, valid);
+    RT_CYC_AFTER(kCycWalk, col.x);
+    return col;
 }
 
 // ---- recursive_raytrace (:1071-1105) -----------------------------------
@@ -1390,6 +1456,7 @@ template <int kDepth, bool kAccum>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
+    RT_CYC(kCycRaygen);
     if (!__any(px.active)) return;
     const int x = px.x, y = px.y, local_row = px.local_row;
     const bool active = px.active;
@@ -1418,6 +1485,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         if constexpr (kDepth == 0) col = trace0(S, ray, active);
         else col = trace_tree<kDepth>(S, ray, active);
 #endif
+        RT_CYC_AFTER(kCycStore, col.x);
         if (active) store_pixel(p, z, idx, col);
     } else {
         const uint32_t pixel = static_cast<uint32_t>(y) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x);
@@ -1517,6 +1585,10 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
 #ifdef RT_STATS
     if (lane < kStats) rt_stats_lds[wave][lane] = 0u;
 #endif
+#ifdef RT_CYCLES
+    if (lane <= kCycPhases) rt_cyc_lds[wave][lane] = lane == kCycPhases ? __builtin_amdgcn_s_memtime() : 0u;
+    if (lane == 0) rt_cyc_cur[wave] = kCycPrologue;
+#endif
     __syncthreads();
     RT_PHASE(13);
     Scene S;
@@ -1570,6 +1642,10 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     RT_PHASE(7);
 #ifdef RT_STATS
     if (lane < kStats) atomicAdd(&rt_stats[lane], static_cast<unsigned long long>(rt_stats_lds[wave][lane]));
+#endif
+#ifdef RT_CYCLES
+    RT_CYC(kCycStore);
+    if (lane < kCycPhases) atomicAdd(&rt_cycles[lane], rt_cyc_lds[wave][lane]);
 #endif
     if (!queued) return;
     if (lane == 0 && atomicAdd(done, 1) == q_waves - 1) {
@@ -1710,6 +1786,19 @@ extern "C" int rt_debug_stats(unsigned long long *dst, int clear) {
         void *ptr = nullptr;
         if (hipGetSymbolAddress(&ptr, HIP_SYMBOL(rtamd::rt_stats)) != hipSuccess) return -1;
         return hipMemset(ptr, 0, sizeof(rtamd::rt_stats)) == hipSuccess ? 0 : -1;
+    }
+    return 0;
+}
+#endif
+#ifdef RT_CYCLES
+extern "C" int rt_debug_cycles(unsigned long long *dst, int clear) {
+    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(rtamd::rt_cycles), sizeof(rtamd::rt_cycles), 0, hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return -1;
+    if (clear) {
+        void *ptr = nullptr;
+        if (hipGetSymbolAddress(&ptr, HIP_SYMBOL(rtamd::rt_cycles)) != hipSuccess) return -1;
+        return hipMemset(ptr, 0, sizeof(rtamd::rt_cycles)) == hipSuccess ? 0 : -1;
     }
     return 0;
 }

@@ -53,3 +53,20 @@ def gpu_ctx():
     ctx = rt.Context(0)
     yield ctx
     ctx.close()
+
+
+def strat_manifest():
+    """Stratified crop sets of the deep configs (tests/golden/make_strat_golden.py)."""
+    with open(os.path.join(GOLDEN, "strat_manifest.json")) as f:
+        return json.load(f)
+
+
+def load_strat(name):
+    """(rgb (n, h, w, 3), crops (n, 4) of (x0, y0, w, h), unproj (4, 4))."""
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    return z["rgb"], z["crops"], z["unproj"].astype(np.float32)
+
+
+def row_bands(crops):
+    """The distinct row ranges (y0, y0 + h) of a crop set."""
+    return sorted({(int(c[1]), int(c[1] + c[3])) for c in crops})

@@ -810,3 +810,39 @@ def test_scene_update_waits_for_renders_on_other_streams(gpu_ctx):
         assert np.array_equal(out.cpu().numpy(), want_a)
     finally:
         sc.close()
+
+
+STRAT = __import__("conftest").strat_manifest()
+
+
+@pytest.mark.parametrize("name", sorted(STRAT))
+def test_stratified_crops_product_path_matches_gl(gpu_ctx, name):
+    """rt_render(cam = NULL, time) — the product path — against the
+    stratified llvmpipe crops of configs 3 and 4 (a grid over the whole
+    frame with its edges and corners, plus the most glass-heavy crops,
+    tests/golden/make_strat_golden.py): bit-exact on every pixel; and the
+    kernel equals the oracle on every full row band the crops lie in."""
+    from conftest import load_strat, row_bands
+    m = STRAT[name]
+    rgb, crops, _ = load_strat(name)
+    objs = scenes.CONFIGS[m["scene"]][0]()
+    w, h, depth = m["width"], m["height"], m["max_depth"]
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        bands = {}
+        for r0, r1 in row_bands(crops):
+            out = np.zeros((r1 - r0, w, 4), np.float32)
+            rc = rt.lib().rt_render(gpu_ctx.handle, sc.handle, None, m["time"], w, h, depth, r0, r1,
+                                    out.ctypes.data, 0, None)
+            assert rc == 0, rt.lib().rt_last_error()
+            bands[(r0, r1)] = out
+    finally:
+        sc.close()
+    for k, (x0, y0, cw, ch) in enumerate(crops):
+        g = bands[(int(y0), int(y0 + ch))][:, x0:x0 + cw]
+        assert (g[..., 3] == 0).all()
+        s = parity_stats(g, rgb[k])
+        assert s["exact"] == 1.0, (name, k, (x0, y0, cw, ch), s)
+    for (r0, r1), g in bands.items():
+        o = oracle_render(objs, w, h, depth, m["time"], rows=(r0, r1))
+        assert np.array_equal(g, o), (name, r0, parity_stats(g, o))

@@ -324,7 +324,7 @@ def test_inv_sqrt_near_one():
 # the development switches rt_kernel.hip keeps (tools/ablate.sh, tools/stats.py,
 # tools/phase_trace.py, the occupancy knobs); every other A/B arm was removed
 # once measured (DESIGN.md §3 keeps the numbers)
-KERNEL_SWITCHES = ["", "-DRT_STATS", "-DRT_PHASE_TRACE", "-DRT_ABLATE_SHADOW", "-DRT_ABLATE_PHONG",
+KERNEL_SWITCHES = ["", "-DRT_STATS", "-DRT_CYCLES", "-DRT_PHASE_TRACE", "-DRT_ABLATE_SHADOW", "-DRT_ABLATE_PHONG",
                    "-DRT_ABLATE_TRACE", "-DRT_ABLATE_RAYGEN", "-DRT_ABLATE_FRAMES", "-DRT_WPE0=7",
                    "-DRT_WPE_DEEP=5", "-DRT_GMASK_TEXELS=32"]
 

@@ -136,3 +136,25 @@ def test_stack_machine_red_guard_unreachable_below_depth_10():
 def test_oracle_rejects_bad_arguments():
     with pytest.raises(ValueError):
         port.render(port.reference_objects(0.0), 0, 10)
+
+
+STRAT = __import__("conftest").strat_manifest()
+
+
+@pytest.mark.parametrize("name", sorted(STRAT))
+def test_stratified_crops_bit_exact(name):
+    """The oracle with its own frame constants against the stratified
+    llvmpipe crops of configs 3 and 4 (tests/golden/make_strat_golden.py:
+    a grid over the whole frame, edges and corners included, plus the most
+    glass-heavy crops; depth-2 / depth-4 recursion, raytrace_compute.glsl:
+    848-1105): bit-exact on every pixel."""
+    from conftest import load_strat, row_bands
+    from oracle import scenes
+    m = STRAT[name]
+    rgb, crops, _ = load_strat(name)
+    objs = scenes.CONFIGS[m["scene"]][0]()
+    bands = {b: port.render(objs, m["width"], m["height"], m["max_depth"], m["time"], rows=b) for b in row_bands(crops)}
+    for k, (x0, y0, w, h) in enumerate(crops):
+        got = bands[(int(y0), int(y0 + h))][:, x0:x0 + w]
+        s = parity_stats(got, rgb[k])
+        assert s["exact"] == 1.0, (name, k, (x0, y0, w, h), s)

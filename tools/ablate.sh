@@ -23,7 +23,7 @@ if [ "${1:-}" = flags ]; then
   build ${2:?name} openglraytracer_amd/csrc "${3:-}"
   exit 0
 fi
-for v in full:"" noshadow:"-DRT_ABLATE_SHADOW" nophong:"-DRT_ABLATE_PHONG" notrace:"-DRT_ABLATE_TRACE" \
+for v in full:"" cycles:"-DRT_CYCLES" stats:"-DRT_STATS" noshadow:"-DRT_ABLATE_SHADOW" nophong:"-DRT_ABLATE_PHONG" notrace:"-DRT_ABLATE_TRACE" \
          noraygen:"-DRT_ABLATE_RAYGEN" noframes:"-DRT_ABLATE_FRAMES"; do
   build ${v%%:*} openglraytracer_amd/csrc "${v#*:}"
 done
