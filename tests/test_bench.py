@@ -42,7 +42,7 @@ def test_config2_two_ranks_row_tiled_gather():
     assert "GL_RGBA8" in line["config"]["output"]
     ranks = line["timing"]["per_rank"]
     assert [r["rank"] for r in ranks] == [0, 1] and all(r["kernel_ms"] > 0 and r["collective_ms"] > 0 for r in ranks)
-    assert line["roofline"]["bytes_per_launch"] == 3 * 1920 * 540 * 4  # 4 B per pixel, half the rows
+    assert line["roofline"]["bytes_per_launch"] == 3 * 1920 * 544 * 4  # 4 B per pixel, rank 0: 68 of 135 8-row blocks
     v = line["verified"]
     assert v["bit_exact"] and v["frames_checked"] == 3 and v["mismatched_pixels"] == 0
     ind = line["independent_frames"]

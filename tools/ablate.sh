@@ -23,7 +23,11 @@ if [ "${1:-}" = flags ]; then
   build ${2:?name} openglraytracer_amd/csrc "${3:-}"
   exit 0
 fi
+# (built in parallel, 4 at a time: each is ~1 min of hipcc)
+n=0
 for v in full:"" cycles:"-DRT_CYCLES" stats:"-DRT_STATS" noshadow:"-DRT_ABLATE_SHADOW" nophong:"-DRT_ABLATE_PHONG" notrace:"-DRT_ABLATE_TRACE" \
          noraygen:"-DRT_ABLATE_RAYGEN" noframes:"-DRT_ABLATE_FRAMES"; do
-  build ${v%%:*} openglraytracer_amd/csrc "${v#*:}"
+  build ${v%%:*} openglraytracer_amd/csrc "${v#*:}" &
+  n=$((n + 1)); [ $((n % 4)) -eq 0 ] && wait
 done
+wait
