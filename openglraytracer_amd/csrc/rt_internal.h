@@ -101,6 +101,16 @@ constexpr int kGMaskMaxSpheres = 256;
                             // (r01); after the ordered BVH 32/48/64: 18.29/17.91/17.73 ms, config 3 1.002/1.005/0.996 ms
 #endif
 constexpr int kGMaskTexels = RT_GMASK_TEXELS;
+// The same wide masks as short candidate lists, one 16-B record per (live
+// light, texel): byte 0 = the number of candidate spheres (0..15), bytes
+// 1..15 = their slots (< 256), ascending; kGListOverflow in byte 0: more than
+// 15 candidates, use the texel's mask words. A query then walks its own list:
+// a wave loops max-over-lanes-of-count times, once per candidate, instead of
+// once per set bit per mask word (the sum over the words of the per-word
+// maxima), from one 16-B load instead of one 8-B load per word.
+constexpr int kGListMax = 15;
+constexpr uint32_t kGListOverflow = 255u;
+static_assert(kGMaskMaxSpheres <= 256, "candidate lists hold sphere slots in bytes");
 // Sphere BVH node (depth-first order; the left child is the next node):
 // lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
 // this subtree (-1: end) and leaf = (count << 24) | first sphere slot (0 for
@@ -159,6 +169,7 @@ struct LaunchParams {
     int32_t off_dmask, dmask_n;  // shadow direction masks (live lights x 6 x n x n), 16-B units; -1: none
     int32_t dmask_bytes;         // bytes per mask: 2, 4 or 8 (at most 16, 32, 64 spheres)
     int32_t off_gmask, gmask_words;  // wide masks in the blob past blob_units (not staged), 16-B units; -1: none
+    int32_t off_glist;               // their candidate lists (kGListMax), 16-B units; -1: none
     int32_t blob_units;      // blob size, 16-B units
     // Monte-Carlo accumulation (render_kernel<D, true>): samples
     // [sample0, sample0 + spp) per pixel, jittered inside the pixel when
@@ -194,7 +205,7 @@ struct DeviceScene {
     int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
     int32_t off_bvh = 0, n_bvh = 0, off_blink = 0, off_cone = 0;
     int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
-    int32_t off_gmask = -1, gmask_words = 0;
+    int32_t off_gmask = -1, gmask_words = 0, off_glist = -1;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
 

@@ -326,6 +326,7 @@ struct Scene {
     const char *dmask;  // [live light][face][row][col] shadow direction masks (nullptr: none)
     int dmask_n, dmask_bytes;
     const uint64_t *gmask;  // wide masks in global memory: [live light][texel][word] (nullptr: none)
+    const uint4 *glist;     // their candidate lists: [live light][texel] (nullptr: none)
     int gwords;
     // The same box and light records in the device blob through the constant
     // address space: a wave-uniform record index becomes scalar loads into
@@ -583,7 +584,7 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
 
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool valid) {
+__device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool valid, int hint) {
     Hit h{10000.0f, -1, 0, 0};
     RT_STAT(kPrimary ? 0 : 1, valid);
     RT_STAT(kPrimary ? 13 : 2, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
@@ -628,6 +629,13 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
         }
     } else if (!kPrimary && S.cull && S.nbvh > 0) {
         // secondary rays: stackless depth-first BVH walk (skip links)
+#ifndef RT_NO_HINT
+        // the sphere the ray starts inside (when its parent's hit says so:
+        // a refraction into or a reflection inside a sphere) first: its exit
+        // bounds the walk's interval at once, so only nodes that overlap
+        // the chord are visited (any order gives the same hit: `closer`)
+        if (hint >= 0) test_sphere(S, hint, r.start, d2, qa2, qa4, floor, false, h);
+#endif
         const RayInv q = ray_inv(r);
         int node = valid ? 0 : -1;
         // while-while: each lane walks nodes until it holds a leaf (or its
@@ -672,9 +680,9 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
     return h;
 }
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
+__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid, int hint = -1) {
     RT_CYC(kPrimary ? kCycClosest1 : kCycClosest2);
-    const Hit h = closest_impl<kPrimary>(S, r, valid);
+    const Hit h = closest_impl<kPrimary>(S, r, valid, hint);
     RT_CYC_AFTER(kCycWalk, h.t);
     return h;
 }
@@ -798,10 +806,33 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
         return hit;
     }
     if (S.gmask) {
-        // wide masks from L2: `mask` holds the texel (-1: every sphere); the
-        // words are read one at a time, each walked like the LDS masks below
+        // wide masks from L2: `mask` holds the texel (-1: every sphere)
         const int texel = static_cast<int>(static_cast<int64_t>(mask));
         const int per_light = 6 * kGMaskTexels * kGMaskTexels;
+        bool ask = need;  // lanes that walk the mask words below
+#ifndef RT_NO_GLIST
+        if (S.glist) {
+            // the texel's candidate list (rt_internal.h kGListMax): one 16-B
+            // load, then one pass per candidate of the longest list — a
+            // wave no longer pays, per mask word, for the lane with the most
+            // candidates in that word
+            uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+            if (need && !hit && texel >= 0) rec = S.glist[static_cast<size_t>(slot) * per_light + texel];
+            uint32_t cnt = rec.x & 0xFFu;
+            const bool wide = need && !hit && (texel < 0 || cnt == kGListOverflow);
+            if (wide) cnt = 0u;
+            for (uint32_t i = 1; __any(i <= cnt); ++i) {  // i: wave-uniform
+                RT_STAT(9, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
+                if (i <= cnt) {
+                    const uint32_t word = i < 4 ? rec.x : (i < 8 ? rec.y : (i < 12 ? rec.z : rec.w));
+                    exact_cand(static_cast<int>((word >> (8 * (i & 3u))) & 0xFFu));
+                    if (hit) cnt = 0u;
+                }
+            }
+            if (!__any(wide)) return hit;
+            ask = wide;  // more than kGListMax candidates, or every sphere: the words
+        }
+#endif
         // every word of the texel requested up front (independent L2 loads
         // in flight together), then walked word by word (one walk over all
         // words at once measured slower: config 3 +7 %, config 4 even)
@@ -812,13 +843,13 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
         for (int w = 0; w < kMaxWords; ++w) {
             // (loading in every lane and selecting measured slower: config 4
             // 16.57 -> 17.16 ms, config 3 +2 %)
-            words[w] = (w < S.gwords && need && !hit && texel >= 0) ? row[w] : ~uint64_t{0};
+            words[w] = (w < S.gwords && ask && !hit && texel >= 0) ? row[w] : ~uint64_t{0};
         }
 #pragma unroll
         for (int w = 0; w < kMaxWords; ++w) {
             if (w >= S.gwords) break;
             uint64_t cand = 0u;
-            if (need && !hit) {
+            if (ask && !hit) {
                 cand = words[w];
                 const int rest = S.ns - 64 * w;
                 if (rest < 64) cand &= (uint64_t{1} << rest) - 1u;
@@ -830,7 +861,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
                     cand = hit ? 0u : cand & (cand - 1u);
                 }
             }
-            if (!__any(need && !hit)) break;
+            if (!__any(ask && !hit)) break;
         }
         return hit;
     }
@@ -1158,6 +1189,7 @@ struct Frame {
     int flags;    // 1: refraction spawned; 2: waiting for the reflection; 4: for the refraction;
                   // | material << 3 (rho and tau read back from it: a 40-B frame instead of
                   // 48, config 4 18.68 -> 18.26 ms, config 3 1.022 -> 1.000 ms)
+                  // | (refraction ray's start sphere + 1) << kHintShift
 };
 
 #ifdef RT_ABLATE_FRAMES
@@ -1202,19 +1234,26 @@ struct Frames {
     __device__ __forceinline__ void set(int level, const Frame &v) { f[level] = v; }
 };
 
-template <int kDepth>
-__device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
+// materials < 256 (RT_MAX_MATERIALS) in flags bits 3-10, sphere slot + 1 < 2048 above
+constexpr int kHintShift = 11;
+static_assert(RT_MAX_MATERIALS <= 256 && RT_MAX_OBJECTS < 2047, "frame flags layout");
+
+// `emit(value)` receives each lane's colour when its tree is finished (the
+// lane then rides along with valid = false): the caller stores the pixel
+// there, so no result registers stay live through the rest of the walk.
+template <int kDepth, class Emit>
+__device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active, Emit &&emit) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
     Frames<kDepth> F;
     int level = 0;
+    int hint = -1;  // the sphere the current ray starts inside, if known (closest)
     bool done = !active;
-    v3 result = black;
     bool first = true;
     while (__any(!done)) {
         RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
         const bool valid = !done;
         const bool primary = first;
-        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
+        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid, hint);
         first = false;
         const bool hit = valid && h.obj >= 0;
         const Collision c = primary ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
@@ -1233,14 +1272,20 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
             fr.rs = sub(c.p, muls(c.n, 0.001f));
             const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
             fr.rd = refract(ray.dir, c.n, ratio);
-            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3);
+            // a sphere hit from outside: the refraction ray starts inside it
+            // (p - 0.001 n); from inside (n flipped): the reflection ray does
+            const int sph = h.slot >= 0 ? h.slot : -1;
+            const int hint_t = c.inside ? -1 : sph, hint_r = c.inside ? sph : -1;
+            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3) | ((hint_t + 1) << kHintShift);
             F.set(level, fr);
             if (sr) {
                 ray.start = add(c.p, muls(c.n, 0.001f));
                 ray.dir = reflect(ray.dir, c.n);
+                hint = hint_r;
             } else {
                 ray.start = fr.rs;
                 ray.dir = fr.rd;
+                hint = hint_t;
             }
             ++level;
             continue;
@@ -1250,7 +1295,7 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
         bool next_child = false;
         while (level > 0 && !next_child) {
             Frame fr = F.get(level - 1);
-            const MatRec &fm = S.mat[fr.flags >> 3];
+            const MatRec &fm = S.mat[(fr.flags >> 3) & 0xFF];
             const float rho = fm.reflectivity, tau = fm.transparency;
             if (fr.flags & 2) {
                 fr.col = mix(fr.col, value, rho);
@@ -1259,6 +1304,7 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
                     F.set(level - 1, fr);
                     ray.start = fr.rs;
                     ray.dir = fr.rd;
+                    hint = (fr.flags >> kHintShift) - 1;
                     next_child = true;
                 } else {
                     value = fr.col;
@@ -1270,11 +1316,10 @@ __device__ __forceinline__ v3 trace_tree(const Scene &S, Ray ray, bool active) {
             }
         }
         if (!next_child) {
-            result = value;
+            emit(value);
             done = true;
         }
     }
-    return result;
 }
 
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
@@ -1290,8 +1335,9 @@ __device__ __forceinline__ uint32_t unorm8(float v) {
     return static_cast<uint32_t>(__builtin_rintf(v * 255.0f));
 }
 
-// One pixel's colour into the launch's surface (float4 or GL_RGBA8 bytes).
-__device__ __forceinline__ void store_pixel(const LaunchParams &p, int z, size_t idx, v3 col) {
+// One pixel's colour into the launch's surface (float4 or GL_RGBA8 bytes);
+// idx = local_row * width + x (< 2^32: 65536 x 65536 frames at most).
+__device__ __forceinline__ void store_pixel(const LaunchParams &p, int z, uint32_t idx, v3 col) {
     const size_t at = static_cast<size_t>(z) * p.n_rows * p.width + idx;
     if (p.out_format == RT_OUTPUT_RGBA8) {  // GL_RGBA8 unorm store of vec4(rgb, 0.0) (main.cpp:223, :404): rt_pack_rgba8
         reinterpret_cast<uint32_t *>(p.out)[at] = unorm8(col.x) | (unorm8(col.y) << 8) | (unorm8(col.z) << 16);
@@ -1471,7 +1517,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         S.ty1 = fy > S.ty1 ? fy : S.ty1;
     }
     float4 *out = p.out + static_cast<size_t>(z) * p.n_rows * p.width;
-    const size_t idx = static_cast<size_t>(local_row) * p.width + x;
+    const uint32_t idx = static_cast<uint32_t>(local_row) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x);
 
     if constexpr (!kAccum) {
         const Ray ray = have_pre ? pre : camera_ray(p, V, x, y, 0.0f, 0.0f);
@@ -1481,9 +1527,12 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 #elif defined(RT_ABLATE_TRACE)
         const v3 col = ray.dir;
 #else
-        v3 col;
-        if constexpr (kDepth == 0) col = trace0(S, ray, active);
-        else col = trace_tree<kDepth>(S, ray, active);
+        if constexpr (kDepth > 0) {
+            // each lane's pixel stored as soon as its tree is finished
+            trace_tree<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
+            return;
+        }
+        const v3 col = trace0(S, ray, active);
 #endif
         RT_CYC_AFTER(kCycStore, col.x);
         if (active) store_pixel(p, z, idx, col);
@@ -1494,9 +1543,9 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
             const uint32_t sid = static_cast<uint32_t>(p.sample0 + smp);
             const float jx = p.jitter ? jitter_u(p.seed, sid, pixel, 0u) : 0.0f;
             const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
-            v3 col;
+            v3 col = mk(0.0f, 0.0f, 0.0f);
             if constexpr (kDepth == 0) col = trace0(S, camera_ray(p, V, x, y, jx, jy), active);
-            else col = trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active);
+            else trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active, [&](v3 c) { col = c; });
             acc = add(acc, col);
         }
         if (active) {
@@ -1611,6 +1660,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // budget and use the per-wave cone for such scenes)
     S.gmask = kDepth >= 2 && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
     S.gwords = p.gmask_words;
+    S.glist = S.gmask && p.off_glist >= 0 ? reinterpret_cast<const uint4 *>(blob + p.off_glist) : nullptr;
     S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
     S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
     S.nbvh = p.n_bvh;

@@ -951,7 +951,9 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     // also beside the LDS masks (depth 0-1 keep those; depth >= 2 reads these),
     // kept in the device blob past the staged part and read through L2.
     std::vector<uint64_t> gmask;
+    std::vector<uint8_t> glist;
     ds.off_gmask = -1;
+    ds.off_glist = -1;
     ds.gmask_words = 0;
 #ifndef RT_GMASK_FROM
 #define RT_GMASK_FROM 32  // wide masks above this many spheres at depth >= 2 (tools/ablate.sh flags; config 3, 64 spheres: 1.15 -> 1.11 ms)
@@ -962,6 +964,23 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         build_direction_masks(sph, smeta, lights, lrec, kGMaskTexels, gmask, ds.gmask_words);
         ds.off_gmask = off;
         off += units(gmask.size() * 8);
+        // the candidate lists of the same texels (rt_internal.h kGListMax)
+        const size_t n_texels = gmask.size() / static_cast<size_t>(ds.gmask_words);
+        glist.assign(n_texels * 16, 0);
+        for (size_t t = 0; t < n_texels; ++t) {
+            uint8_t *rec = glist.data() + t * 16;
+            int n = 0;
+            for (int w = 0; w < ds.gmask_words; ++w)
+                for (uint64_t bits = gmask[t * ds.gmask_words + w]; bits; bits &= bits - 1) {
+                    const int s = 64 * w + __builtin_ctzll(bits);
+                    if (s >= static_cast<int>(sph.size())) break;
+                    if (n < kGListMax) rec[1 + n] = static_cast<uint8_t>(s);
+                    ++n;
+                }
+            rec[0] = n <= kGListMax ? static_cast<uint8_t>(n) : static_cast<uint8_t>(kGListOverflow);
+        }
+        ds.off_glist = off;
+        off += units(glist.size());
     }
     ds.n_spheres = static_cast<int32_t>(sph.size());
     ds.n_boxes = static_cast<int32_t>(boxes.size());
@@ -982,6 +1001,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     if (ds.off_cone >= 0) put(ds.off_cone, cones.data(), cones.size() * sizeof(ShadowCone));
     if (ds.off_dmask >= 0) put(ds.off_dmask, dmask_bytes.data(), dmask_bytes.size());
     if (ds.off_gmask >= 0) put(ds.off_gmask, gmask.data(), gmask.size() * 8);
+    if (ds.off_glist >= 0) put(ds.off_glist, glist.data(), glist.size());
     return RT_OK;
 }
 

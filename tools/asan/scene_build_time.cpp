@@ -41,6 +41,20 @@ int main() {
         std::vector<float4> blob;
         rtamd::DeviceScene ds;
         rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds);
+        if (ds.off_glist >= 0) {  // candidate-list lengths of the wide masks (rt_internal.h kGListMax)
+            const unsigned char *g = reinterpret_cast<const unsigned char *>(blob.data()) + 16L * ds.off_glist;
+            const long texels = (static_cast<long>(blob.size()) - ds.off_glist);
+            long over = 0, hist[4] = {0, 0, 0, 0};
+            double sum = 0;
+            for (long t = 0; t < texels; ++t) {
+                const int c = g[16 * t];
+                if (c == 255) { ++over; continue; }
+                sum += c;
+                ++hist[c == 0 ? 0 : (c <= 2 ? 1 : (c <= 7 ? 2 : 3))];
+            }
+            std::printf("room + %3d spheres: %ld texel lists, mean length %.2f, 0: %ld, 1-2: %ld, 3-7: %ld, 8-15: %ld, "
+                        "overflow (> 15): %ld\n", n, texels, sum / (texels - over), hist[0], hist[1], hist[2], hist[3], over);
+        }
         // LDS per work-group: the staged blob + per-sphere camera terms and footprints + per-box camera terms
         const long lds = 16L * (ds.blob_units + 2L * n + 1);
         std::printf("room + %3d spheres: scene build %.3f ms (median of 7), blob %016llx, LDS %ld B (masks %d B)\n", n,

@@ -2,7 +2,7 @@
 
     python tools/phase_trace.py [CONFIG] [BUILD]
 
-BUILD (default "phase") is a tools/_ablate build made with
+BUILD (default "phase") is an _ab build made with
 `tools/ablate.sh flags phase "-DRT_PHASE_TRACE -DRT_WPE0=8"` (the probe
 costs two VGPRs; RT_WPE0=8 keeps the product build's 8 waves/SIMD): lane 0 of every wave records
 the 100 MHz real-time clock at kernel entry (0), after the prologue barrier
@@ -25,7 +25,7 @@ from oracle import scenes
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "config2"
 name = sys.argv[2] if len(sys.argv) > 2 else "phase"
-L = C.CDLL(os.path.join(ROOT, "tools", "_ablate", name, "libopenglraytracer_amd.so"))
+L = C.CDLL(os.path.join(ROOT, "_ab", name, "libopenglraytracer_amd.so"))
 vp, i = C.c_void_p, C.c_int
 L.rt_create.argtypes = [i, vp]
 L.rt_scene_create.argtypes = [vp, vp, i, vp, i, vp, i, vp]

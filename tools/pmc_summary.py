@@ -64,6 +64,7 @@ if os.path.exists(blog):
             except ValueError:
                 pass
 w, f, sq, cyc = counters("pmc_write"), counters("pmc_fetch"), counters("pmc_sq"), counters("pmc_cyc")
+l2 = counters("pmc_l2")
 write_b = mean(w.get("WRITE_SIZE", [])) * 1024 if w.get("WRITE_SIZE") else None
 fetch_b = mean(f.get("FETCH_SIZE", [])) * 1024 * 2 if f.get("FETCH_SIZE") else None
 out = {
@@ -82,6 +83,8 @@ out = {
     "sq_busy_cycles_per_launch": mean(cyc.get("SQ_BUSY_CYCLES", [])),
     "sq_wait_inst_any_per_launch": mean(cyc.get("SQ_WAIT_INST_ANY", [])),
     "grbm_gui_active_per_launch": mean(cyc.get("GRBM_GUI_ACTIVE", [])),
+    "l2_hit_per_launch": mean(l2.get("TCC_HIT_sum", [])),
+    "l2_miss_per_launch": mean(l2.get("TCC_MISS_sum", [])),
     "notes": "WRITE_SIZE*1024 exact for 16-B/lane stores; FETCH_SIZE*1024*2 (gfx950 half-count); "
              "GRBM_GUI_ACTIVE summed over 8 XCDs",
 }
@@ -91,8 +94,11 @@ if out["sq_insts_valu_per_launch"] and out["avg_kernel_ns"]:
     # wave64 VALU issue: 2 cycles per instruction per SIMD, 1024 SIMDs
     clk = out.get("effective_clock_ghz") or 2.4
     out["valu_issue_utilisation"] = out["sq_insts_valu_per_launch"] * 2 / (1024 * clk * out["avg_kernel_ns"])
+if out["l2_hit_per_launch"] is not None and out["l2_miss_per_launch"] is not None:
+    tot = out["l2_hit_per_launch"] + out["l2_miss_per_launch"]
+    out["l2_hit_rate"] = out["l2_hit_per_launch"] / tot if tot else None
 allc = {}
-for name in ("pmc_write", "pmc_fetch", "pmc_sq", "pmc_cyc"):
+for name in ("pmc_write", "pmc_fetch", "pmc_sq", "pmc_cyc", "pmc_l2"):
     for cname, vals in counters(name).items():
         allc[cname] = mean(vals)
 out["counters_per_launch"] = allc
