@@ -584,7 +584,7 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
 
 // get_closest_collision (:738-782). Called with all lanes active.
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool valid, int hint) {
+__device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool valid) {
     Hit h{10000.0f, -1, 0, 0};
     RT_STAT(kPrimary ? 0 : 1, valid);
     RT_STAT(kPrimary ? 13 : 2, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
@@ -629,13 +629,10 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
         }
     } else if (!kPrimary && S.cull && S.nbvh > 0) {
         // secondary rays: stackless depth-first BVH walk (skip links)
-#ifndef RT_NO_HINT
-        // the sphere the ray starts inside (when its parent's hit says so:
-        // a refraction into or a reflection inside a sphere) first: its exit
-        // bounds the walk's interval at once, so only nodes that overlap
-        // the chord are visited (any order gives the same hit: `closer`)
-        if (hint >= 0) test_sphere(S, hint, r.start, d2, qa2, qa4, floor, false, h);
-#endif
+        // (testing first the sphere a secondary ray starts inside — a
+        // refraction into or a reflection inside a sphere — changed no node
+        // test: the ordered walk reaches its leaf first anyway; config 4
+        // +1.3 %, config 3 +1.6 %, r03c)
         const RayInv q = ray_inv(r);
         int node = valid ? 0 : -1;
         // while-while: each lane walks nodes until it holds a leaf (or its
@@ -680,9 +677,9 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
     return h;
 }
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid, int hint = -1) {
+__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
     RT_CYC(kPrimary ? kCycClosest1 : kCycClosest2);
-    const Hit h = closest_impl<kPrimary>(S, r, valid, hint);
+    const Hit h = closest_impl<kPrimary>(S, r, valid);
     RT_CYC_AFTER(kCycWalk, h.t);
     return h;
 }
@@ -810,12 +807,13 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
         const int texel = static_cast<int>(static_cast<int64_t>(mask));
         const int per_light = 6 * kGMaskTexels * kGMaskTexels;
         bool ask = need;  // lanes that walk the mask words below
-#ifndef RT_NO_GLIST
         if (S.glist) {
             // the texel's candidate list (rt_internal.h kGListMax): one 16-B
             // load, then one pass per candidate of the longest list — a
             // wave no longer pays, per mask word, for the lane with the most
-            // candidates in that word
+            // candidates in that word (against the words alone: config 4
+            // 16.63 -> 14.83 ms, config 3 0.940 -> 0.896 ms, r03c; the
+            // wave's candidate passes per tile 68.8 -> 52.5)
             uint4 rec = make_uint4(0u, 0u, 0u, 0u);
             if (need && !hit && texel >= 0) rec = S.glist[static_cast<size_t>(slot) * per_light + texel];
             uint32_t cnt = rec.x & 0xFFu;
@@ -832,7 +830,6 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
             if (!__any(wide)) return hit;
             ask = wide;  // more than kGListMax candidates, or every sphere: the words
         }
-#endif
         // every word of the texel requested up front (independent L2 loads
         // in flight together), then walked word by word (one walk over all
         // words at once measured slower: config 3 +7 %, config 4 even)
@@ -1189,7 +1186,6 @@ struct Frame {
     int flags;    // 1: refraction spawned; 2: waiting for the reflection; 4: for the refraction;
                   // | material << 3 (rho and tau read back from it: a 40-B frame instead of
                   // 48, config 4 18.68 -> 18.26 ms, config 3 1.022 -> 1.000 ms)
-                  // | (refraction ray's start sphere + 1) << kHintShift
 };
 
 #ifdef RT_ABLATE_FRAMES
@@ -1234,10 +1230,6 @@ struct Frames {
     __device__ __forceinline__ void set(int level, const Frame &v) { f[level] = v; }
 };
 
-// materials < 256 (RT_MAX_MATERIALS) in flags bits 3-10, sphere slot + 1 < 2048 above
-constexpr int kHintShift = 11;
-static_assert(RT_MAX_MATERIALS <= 256 && RT_MAX_OBJECTS < 2047, "frame flags layout");
-
 // `emit(value)` receives each lane's colour when its tree is finished (the
 // lane then rides along with valid = false): the caller stores the pixel
 // there, so no result registers stay live through the rest of the walk.
@@ -1246,14 +1238,13 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
     const v3 black = mk(0.0f, 0.0f, 0.0f);
     Frames<kDepth> F;
     int level = 0;
-    int hint = -1;  // the sphere the current ray starts inside, if known (closest)
     bool done = !active;
     bool first = true;
     while (__any(!done)) {
         RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
         const bool valid = !done;
         const bool primary = first;
-        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid, hint);
+        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
         first = false;
         const bool hit = valid && h.obj >= 0;
         const Collision c = primary ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
@@ -1272,20 +1263,14 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
             fr.rs = sub(c.p, muls(c.n, 0.001f));
             const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
             fr.rd = refract(ray.dir, c.n, ratio);
-            // a sphere hit from outside: the refraction ray starts inside it
-            // (p - 0.001 n); from inside (n flipped): the reflection ray does
-            const int sph = h.slot >= 0 ? h.slot : -1;
-            const int hint_t = c.inside ? -1 : sph, hint_r = c.inside ? sph : -1;
-            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3) | ((hint_t + 1) << kHintShift);
+            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3);
             F.set(level, fr);
             if (sr) {
                 ray.start = add(c.p, muls(c.n, 0.001f));
                 ray.dir = reflect(ray.dir, c.n);
-                hint = hint_r;
             } else {
                 ray.start = fr.rs;
                 ray.dir = fr.rd;
-                hint = hint_t;
             }
             ++level;
             continue;
@@ -1295,7 +1280,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
         bool next_child = false;
         while (level > 0 && !next_child) {
             Frame fr = F.get(level - 1);
-            const MatRec &fm = S.mat[(fr.flags >> 3) & 0xFF];
+            const MatRec &fm = S.mat[fr.flags >> 3];
             const float rho = fm.reflectivity, tau = fm.transparency;
             if (fr.flags & 2) {
                 fr.col = mix(fr.col, value, rho);
@@ -1304,7 +1289,6 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
                     F.set(level - 1, fr);
                     ray.start = fr.rs;
                     ray.dir = fr.rd;
-                    hint = (fr.flags >> kHintShift) - 1;
                     next_child = true;
                 } else {
                     value = fr.col;
