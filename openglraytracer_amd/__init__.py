@@ -222,6 +222,11 @@ class Context:
         (default), else derived by every work-group (output identical)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_FRAME_CONSTS, 1 if on else 0))
 
+    def set_wavefront(self, on):
+        """RT_OPT_WAVEFRONT: depth >= 2 frames level by level from ray queues
+        (default) instead of the per-pixel depth-first walk (output identical)."""
+        _check(lib().rt_context_set(self._h, abi.RT_OPT_WAVEFRONT, 1 if on else 0))
+
     def set_output(self, fmt):
         """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel),
         abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)

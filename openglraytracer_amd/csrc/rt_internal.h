@@ -189,11 +189,28 @@ struct LaunchParams {
     // (host_frame_setup): n_frame_consts records per view, view k's at
     // k * n_frame_consts; 0: every work-group derives them.
     int32_t n_frame_consts;
+    // Rows [slice_begin, slice_begin + slice_rows) of the launch's local rows
+    // (the whole launch when slice_rows = 0); a wavefront frame runs slice by slice.
+    int32_t slice_begin, slice_rows;
+    // Wavefront path (depth >= 2, rt_kernel.hip launch_wavefront): the work
+    // buffer (wf_layout), its capacity in pixels of a slice, the frame's max
+    // depth and the level a trace / mix launch processes. nullptr: megakernel.
+    void *wf_base;
+    int32_t wf_cap, wf_depth, wf_level;
     float4 frame_consts[kMaxFrameConsts];
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
 // MI355X); this block stays under 6 KiB.
 static_assert(sizeof(LaunchParams) <= 6144, "kernel argument block");
+// Wavefront work buffer for a slice of P pixels at max depth D (rt_kernel.hip):
+// 256 B of counters, the level-0 nodes (P), then per level L = 1..D the rays
+// and nodes of reflection and of refraction children, P * 2^(L-1) each
+// (every node has at most one child of each kind); 32 B per ray and per node.
+constexpr size_t kWfCounters = 256;
+constexpr size_t kWfRecord = 32;
+inline size_t wf_bytes_per_pixel(int depth) { return kWfRecord * (1 + 4 * ((size_t{1} << depth) - 1)); }
+inline size_t wf_buffer_bytes(int64_t pixels, int depth) { return kWfCounters + pixels * wf_bytes_per_pixel(depth); }
+constexpr size_t kWfBudget = size_t{8} << 30;  // work buffer of a context, at most (8 GiB of the GPU's 288)
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
 constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
 constexpr int kSchedInts = 2 * kQueues * kQueueStride; // heads + done counters of one launch
@@ -261,6 +278,11 @@ struct rt_context {
     int timing = 1;   // RT_OPT_TIMING
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int host_consts = 1;  // RT_OPT_FRAME_CONSTS
+    int wavefront = 1;    // RT_OPT_WAVEFRONT: depth >= 2 frames level by level (rt_kernel.hip)
+    void *wf_buf = nullptr;  // its work buffer (grown on demand)
+    size_t wf_bytes = 0;
+    hipEvent_t wf_done = nullptr;  // recorded after the last wavefront render (launches on other streams wait)
+    bool wf_used = false;
     int n_cu = 0;               // compute units of the device
     int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
     unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots

@@ -1438,9 +1438,9 @@ __device__ __forceinline__ Pixel wave_pixel(const LaunchParams &p, int wx, int w
     const int lane = threadIdx.x & 63;
     Pixel px;
     px.x = wx * 8 + (lane & 7);
-    px.local_row = wy * 8 + (lane >> 3);
-    px.active = px.x < p.width && px.local_row < p.n_rows;
-    px.y = output_row(p, px.active ? px.local_row : wy * 8);
+    px.local_row = p.slice_begin + wy * 8 + (lane >> 3);
+    px.active = px.x < p.width && px.local_row < p.slice_begin + p.slice_rows;
+    px.y = output_row(p, px.active ? px.local_row : p.slice_begin + wy * 8);
     return px;
 }
 
@@ -1479,10 +1479,114 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
     return ray;
 }
 
+
+// ---- wavefront path for deep trees (max_depth >= 2) ----------------------
+// The stack machine (:848-1105) gives every node of a pixel's ray tree the
+// value mix(mix(phong, R, rho), T, tau) of its own Phong colour and its
+// children's values (each mix only for a spawned child, a missed ray black):
+// a node's value depends on its subtree alone, not on the order the tree is
+// walked. So instead of one depth-first walk per lane (trace_tree: frames in
+// scratch, every lane at its own tree position), a frame runs level by level:
+//  * level 0 (render_kernel<2, false, true>): the camera rays of the tiled
+//    kernel; a pixel whose hit spawns no child is stored at once, the others
+//    become level-0 nodes and push their children (wf_children);
+//  * levels 1..D (wf_trace_kernel): persistent waves take 64 rays at a time
+//    from the level's queues — reflection rays first, then refraction rays,
+//    each queue in the order its parents' waves pushed them, so a wave traces
+//    rays of one kind from neighbouring pixels — trace, shade, store their
+//    node and push the next level's children;
+//  * levels D-1..0 (wf_mix_kernel): every node with children mixes its
+//    children's final values into its own, bottom-up; level 0 stores the pixel.
+// Same device functions, same operations per node: bit-identical to
+// trace_tree (tests/test_gpu_parity.py renders both).
+// Nodes and rays are 32-B records in the context's work buffer
+// (rt_internal.h wf_buffer_bytes); counters: per level and kind the number
+// of rays / nodes (ints 2L + kind), per level the queue head (int 32 + L).
+struct WfRay {
+    float4 o, d;  // start, direction (w unused)
+};
+struct WfNode {
+    float4 col;  // xyz: the node's value (phong, black on a miss; mixed in place), w: meta bits
+    int4 link;   // reflection child, refraction child (-1: none), level 0: the pixel's output index
+};
+constexpr uint32_t kWfSr = 1u << 8, kWfSt = 1u << 9;  // meta: material | spawned children
+__device__ __forceinline__ int *wf_counters(const LaunchParams &p) { return static_cast<int *>(p.wf_base); }
+__device__ __forceinline__ char *wf_level_base(const LaunchParams &p, int level) {
+    const size_t P = static_cast<size_t>(p.wf_cap);
+    return static_cast<char *>(p.wf_base) + kWfCounters + kWfRecord * P +
+           4 * kWfRecord * P * ((size_t{1} << (level - 1)) - 1);
+}
+__device__ __forceinline__ WfRay *wf_rays(const LaunchParams &p, int level, int kind) {
+    const size_t cap = static_cast<size_t>(p.wf_cap) << (level - 1);
+    return reinterpret_cast<WfRay *>(wf_level_base(p, level) + kind * kWfRecord * cap);
+}
+__device__ __forceinline__ WfNode *wf_nodes(const LaunchParams &p, int level, int kind) {
+    if (level == 0) return reinterpret_cast<WfNode *>(static_cast<char *>(p.wf_base) + kWfCounters);
+    const size_t cap = static_cast<size_t>(p.wf_cap) << (level - 1);
+    return reinterpret_cast<WfNode *>(wf_level_base(p, level) + (2 + kind) * kWfRecord * cap);
+}
+// Wave-aggregated append (all lanes active): one atomic per wave; the lanes
+// with `want` get consecutive slots in lane order, the others -1.
+__device__ __forceinline__ int wave_append(int *counter, bool want) {
+    const uint64_t m = __ballot(want);
+    if (!m) return -1;
+    const int lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
+    int base = 0;
+    if (lane == lead) base = atomicAdd(counter, __popcll(m));
+    base = __builtin_amdgcn_readlane(base, lead);
+    return want ? base + static_cast<int>(__popcll(m & ((uint64_t{1} << lane) - 1u))) : -1;
+}
+// Push the children of this lane's node at `level` to level + 1 (the rays
+// trace_tree would start: :979-1030) and return their slots.
+__device__ __forceinline__ void wf_children(const LaunchParams &p, const Scene &S, int level, const Ray &ray,
+                                            const Collision &c, bool sr, bool st, int &cr, int &ct) {
+    int *cnt = wf_counters(p);
+    cr = wave_append(cnt + 2 * (level + 1), sr);
+    ct = wave_append(cnt + 2 * (level + 1) + 1, st);
+    if (sr) {
+        const v3 o = add(c.p, muls(c.n, 0.001f)), d = reflect(ray.dir, c.n);
+        wf_rays(p, level + 1, 0)[cr] = {make_float4(o.x, o.y, o.z, 0.0f), make_float4(d.x, d.y, d.z, 0.0f)};
+    }
+    if (st) {
+        const MatRec &m = S.mat[c.material];
+        const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
+        const v3 o = sub(c.p, muls(c.n, 0.001f)), d = refract(ray.dir, c.n, ratio);
+        wf_rays(p, level + 1, 1)[ct] = {make_float4(o.x, o.y, o.z, 0.0f), make_float4(d.x, d.y, d.z, 0.0f)};
+    }
+}
+// One ray per lane at `level` (all lanes active): closest hit, Phong, the
+// node's value and children. `store(value)`: a lane whose node spawns no
+// child at level 0 (its pixel is final); `node(value, meta, cr, ct)`: every
+// other lane with a ray (level 0: those that spawn).
+template <bool kPrimary, class Store, class Node>
+__device__ __forceinline__ void wf_trace(const LaunchParams &p, const Scene &S, int level, const Ray &ray, bool valid,
+                                         Store &&store, Node &&node) {
+    const v3 black = mk(0.0f, 0.0f, 0.0f);
+    const Hit h = closest<kPrimary>(S, ray, valid);
+    const bool hit = valid && h.obj >= 0;
+    Collision c;
+    c.material = 0;
+    v3 col = black;
+    bool sr = false, st = false;
+    if (__any(hit)) {
+        c = resolve<kPrimary>(S, ray, h, hit);
+        col = phong(S, ray, c, hit);
+        const MatRec &m = S.mat[c.material];
+        sr = hit && level < p.wf_depth && m.reflectivity > 0.0f;
+        st = hit && level < p.wf_depth && m.transparency > 0.0f;
+    }
+    const v3 value = hit ? col : black;  // a missed ray is black (:962-963)
+    int cr = -1, ct = -1;
+    if (__any(sr || st)) wf_children(p, S, level, ray, c, sr, st, cr, ct);
+    const uint32_t meta = static_cast<uint32_t>(c.material) | (sr ? kWfSr : 0u) | (st ? kWfSt : 0u);
+    if (kPrimary && valid && !(sr || st)) store(value);
+    if (valid && (!kPrimary || sr || st)) node(value, meta, cr, ct);
+}
+
 // One 8x8 wave tile (wx, wy) of view z: lane l renders pixel (8 wx + l % 8,
 // 8 wy + l / 8). `pre`: the lane's camera ray, already computed (the tiled
 // path computes it while the scene is staged), or nullptr.
-template <int kDepth, bool kAccum>
+template <int kDepth, bool kAccum, bool kWf>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
@@ -1490,7 +1594,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
     if (!__any(px.active)) return;
     const int x = px.x, y = px.y, local_row = px.local_row;
     const bool active = px.active;
-    const int lr0 = wy * 8;
+    const int lr0 = p.slice_begin + wy * 8;
     S.tx0 = wx * 8;
     S.tx1 = S.tx0 + 7;
     S.ty0 = INT_MAX;
@@ -1511,6 +1615,18 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 #elif defined(RT_ABLATE_TRACE)
         const v3 col = ray.dir;
 #else
+        if constexpr (kWf) {
+            // level 0 of a wavefront frame: pixels without children stored,
+            // the others become level-0 nodes (their output index kept)
+            wf_trace<true>(
+                p, S, 0, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); },
+                [&](v3 col, uint32_t meta, int cr, int ct) {
+                    const int n = wave_append(wf_counters(p), true);
+                    wf_nodes(p, 0, 0)[n] = {make_float4(col.x, col.y, col.z, __uint_as_float(meta)),
+                                            make_int4(cr, ct, static_cast<int>(idx), 0)};
+                });
+            return;
+        }
         if constexpr (kDepth > 0) {
             // each lane's pixel stored as soon as its tree is finished
             trace_tree<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
@@ -1563,10 +1679,10 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 // 52 -> 67 us, 8-frame launches, tiled either way, 41.5 -> 50.6 us per frame)
 constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 
-template <int kDepth, bool kAccum>
+template <int kDepth, bool kAccum, bool kWf = false>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    const bool queued = kQueuedDepth(kDepth) && p.sched != nullptr;
+    const bool queued = kQueuedDepth(kDepth) && !kWf && p.sched != nullptr;
     const int z = queued ? 0 : static_cast<int>(blockIdx.z);
     const FrameView &V = p.view[z];
     // wave index through readfirstlane: provably wave-uniform to the compiler,
@@ -1653,7 +1769,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.nl = p.n_lights;
     S.nm = p.n_mats;
     const int wtx = (p.width + 7) / 8;
-    const int total = queued ? wtx * ((p.n_rows + 7) / 8) : 1;
+    const int total = queued ? wtx * ((p.slice_rows + 7) / 8) : 1;
     const int g = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave;  // global wave
     const int n_waves = static_cast<int>(gridDim.x) * (kThreads / 64);
     const int q = g % kQueues;
@@ -1669,8 +1785,8 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
         int nxt = 0;
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
         const int wx = queued ? t % wtx : own_wx, wy = queued ? t / wtx : own_wy;
-        render_wave_tile<kDepth, kAccum>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
-                                         own_ray, !(queued || kAccum));
+        render_wave_tile<kDepth, kAccum, kWf>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
+                                              own_ray, !(queued || kAccum));
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
     RT_PHASE(7);
@@ -1685,6 +1801,126 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     if (lane == 0 && atomicAdd(done, 1) == q_waves - 1) {
         atomicExch(head, 0);  // every wave of the queue has made its last fetch
         atomicExch(done, 0);
+    }
+}
+
+#ifndef RT_WPE_WF
+#define RT_WPE_WF 6
+#endif
+// Levels 1..D of a wavefront frame (see wf_trace): a grid of resident
+// work-groups, each staging the scene blob into LDS once; every wave then
+// takes 64-ray chunks of the level's queues (reflection rays, then
+// refraction rays) from the level's head counter until both are drained.
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WPE_WF))) void wf_trace_kernel(
+    LaunchParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    const float4 *blob = static_cast<const float4 *>(p.scene);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < p.blob_units; i += kThreads) lds[i] = blob[i];
+#ifdef RT_STATS
+    if (lane < kStats) rt_stats_lds[wave][lane] = 0u;
+#endif
+#ifdef RT_CYCLES
+    if (lane <= kCycPhases) rt_cyc_lds[wave][lane] = lane == kCycPhases ? __builtin_amdgcn_s_memtime() : 0u;
+    if (lane == 0) rt_cyc_cur[wave] = kCycPrologue;
+#endif
+    __syncthreads();
+    Scene S;
+    S.sph = lds + p.off_spheres;
+    S.smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
+    S.sph_cam = nullptr;  // (camera-origin terms: primary rays only)
+    S.sph_px = nullptr;
+    S.box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
+    S.box_cam = nullptr;
+    S.mat = reinterpret_cast<const MatRec *>(lds + p.off_mats);
+    S.light = reinterpret_cast<const LightRec *>(lds + p.off_lights);
+    S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
+    S.bvh = lds + p.off_bvh;
+    S.blink = reinterpret_cast<const uint32_t *>(lds + p.off_blink);
+    S.cone = p.off_cone >= 0 ? reinterpret_cast<const ShadowCone *>(lds + p.off_cone) : nullptr;
+    S.dmask = p.off_dmask >= 0 ? reinterpret_cast<const char *>(lds + p.off_dmask) : nullptr;
+    S.dmask_n = p.dmask_n;
+    S.dmask_bytes = p.dmask_bytes;
+    S.gmask = p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
+    S.gwords = p.gmask_words;
+    S.glist = S.gmask && p.off_glist >= 0 ? reinterpret_cast<const uint4 *>(blob + p.off_glist) : nullptr;
+    S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
+    S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
+    S.nbvh = p.n_bvh;
+    S.ns = p.n_spheres;
+    S.nb = p.n_boxes;
+    S.nl = p.n_lights;
+    S.nm = p.n_mats;
+    S.cull = p.view[0].cull;
+    S.tx0 = S.tx1 = S.ty0 = S.ty1 = 0;
+    const int level = p.wf_level;
+    int *cnt = wf_counters(p);
+    const int n_r = __builtin_amdgcn_readfirstlane(cnt[2 * level]), n_t = __builtin_amdgcn_readfirstlane(cnt[2 * level + 1]);
+    const int chunks_r = (n_r + 63) / 64, chunks = chunks_r + (n_t + 63) / 64;
+    int *head = cnt + 32 + level;
+    int chunk = 0;
+    if (lane == 0) chunk = atomicAdd(head, 1);
+    chunk = __builtin_amdgcn_readfirstlane(chunk);
+    while (chunk < chunks) {
+        int nxt = 0;
+        if (lane == 0) nxt = atomicAdd(head, 1);  // fetched one chunk ahead
+        const int kind = chunk < chunks_r ? 0 : 1;
+        const int i = (chunk - (kind ? chunks_r : 0)) * 64 + lane;
+        const bool valid = i < (kind ? n_t : n_r);
+        Ray ray{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 1.0f)};
+        if (valid) {
+            const WfRay r = wf_rays(p, level, kind)[i];
+            ray.start = mk(r.o.x, r.o.y, r.o.z);
+            ray.dir = mk(r.d.x, r.d.y, r.d.z);
+        }
+        WfNode *nodes = wf_nodes(p, level, kind);
+        wf_trace<false>(
+            p, S, level, ray, valid, [](v3) {},
+            [&](v3 col, uint32_t meta, int cr, int ct) {
+                nodes[i] = {make_float4(col.x, col.y, col.z, __uint_as_float(meta)), make_int4(cr, ct, 0, 0)};
+            });
+        chunk = __builtin_amdgcn_readfirstlane(nxt);
+    }
+#ifdef RT_STATS
+    if (lane < kStats) atomicAdd(&rt_stats[lane], static_cast<unsigned long long>(rt_stats_lds[wave][lane]));
+#endif
+#ifdef RT_CYCLES
+    RT_CYC(kCycStore);
+    if (lane < kCycPhases) atomicAdd(&rt_cycles[lane], rt_cyc_lds[wave][lane]);
+#endif
+    (void)wave;
+}
+
+// Levels D-1..0 of a wavefront frame, bottom-up: every node with children
+// takes mix(mix(value, R, rho), T, tau) over its spawned children (whose
+// values are final: their level ran before) (:1034-1054); level 0 stores
+// the pixel.
+__global__ __launch_bounds__(kThreads) void wf_mix_kernel(LaunchParams p) {
+    const int level = p.wf_level;
+    const MatRec *mat = reinterpret_cast<const MatRec *>(static_cast<const float4 *>(p.scene) + p.off_mats);
+    const int *cnt = wf_counters(p);
+    const int n0 = cnt[2 * level], n1 = level == 0 ? 0 : cnt[2 * level + 1];
+    const int stride = static_cast<int>(gridDim.x) * kThreads;
+    for (int g = static_cast<int>(blockIdx.x) * kThreads + static_cast<int>(threadIdx.x); g < n0 + n1; g += stride) {
+        const int kind = g < n0 ? 0 : 1, i = kind ? g - n0 : g;
+        WfNode *nodes = wf_nodes(p, level, kind);
+        const WfNode nd = nodes[i];
+        const uint32_t meta = __float_as_uint(nd.col.w);
+        if (!(meta & (kWfSr | kWfSt))) continue;
+        const MatRec &m = mat[meta & 0xFFu];
+        v3 value = mk(nd.col.x, nd.col.y, nd.col.z);
+        if (meta & kWfSr) {
+            const float4 r = wf_nodes(p, level + 1, 0)[nd.link.x].col;
+            value = mix(value, mk(r.x, r.y, r.z), m.reflectivity);
+        }
+        if (meta & kWfSt) {
+            const float4 t = wf_nodes(p, level + 1, 1)[nd.link.y].col;
+            value = mix(value, mk(t.x, t.y, t.z), m.transparency);
+        }
+        if (level == 0)
+            store_pixel(p, 0, static_cast<uint32_t>(nd.link.z), value);
+        else
+            nodes[i].col = make_float4(value.x, value.y, value.z, nd.col.w);
     }
 }
 
@@ -1714,8 +1950,8 @@ template <int kDepth, bool kAccum>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
     const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
-    dim3 grid((p.width + kTileX - 1) / kTileX, (p.n_rows + kTileY - 1) / kTileY, p.n_views);
-    const int wave_tiles = ((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
+    dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, p.n_views);
+    const int wave_tiles = ((p.width + 7) / 8) * ((p.slice_rows + 7) / 8);
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
     // queued: more wave tiles than resident waves, and every queue has a
     // wave (a queue without one would leave its tiles unrendered)
@@ -1727,6 +1963,37 @@ hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     }
     hipLaunchKernelGGL((render_kernel<kDepth, kAccum>), grid, dim3(kThreads), lds, stream, p);
     return hipGetLastError();
+}
+
+// A wavefront frame (wf_trace): per slice of whole 8-row bands that fits the
+// work buffer (p.wf_cap pixels), the counters cleared, level 0, levels 1..D,
+// then the mixes D-1..0 — all queued on `stream`.
+hipError_t launch_wavefront(LaunchParams &p, int depth, hipStream_t stream) {
+    const int slice_rows = std::max(8, p.wf_cap / p.width / 8 * 8);
+    const size_t lds0 = lds_bytes(p), lds1 = static_cast<size_t>(p.blob_units) * sizeof(float4);
+    const void *trace_fn = reinterpret_cast<const void *>(&wf_trace_kernel);
+    const int resident = std::max(1, groups_per_cu(trace_fn, lds1) * std::max(p.n_cu, 1));
+    const int mix_groups = std::max(1, 8 * std::max(p.n_cu, 1));
+    p.sched = nullptr;
+    p.wf_level = 0;
+    for (int begin = 0; begin < p.n_rows; begin += slice_rows) {
+        p.slice_begin = begin;
+        p.slice_rows = std::min(slice_rows, p.n_rows - begin);
+        hipError_t e = hipMemsetAsync(p.wf_base, 0, kWfCounters, stream);
+        if (e != hipSuccess) return e;
+        const dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, 1);
+        hipLaunchKernelGGL((render_kernel<2, false, true>), grid, dim3(kThreads), lds0, stream, p);
+        for (int level = 1; level <= depth; ++level) {
+            p.wf_level = level;
+            hipLaunchKernelGGL(wf_trace_kernel, dim3(resident), dim3(kThreads), lds1, stream, p);
+        }
+        for (int level = depth - 1; level >= 0; --level) {
+            p.wf_level = level;
+            hipLaunchKernelGGL(wf_mix_kernel, dim3(mix_groups), dim3(kThreads), 0, stream, p);
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 template <int kDepth>
@@ -1742,6 +2009,12 @@ size_t lds_bytes(const LaunchParams &p) {
 }
 
 hipError_t launch_render(LaunchParams &p, int max_depth, hipStream_t stream) {
+    if (p.slice_rows <= 0) {  // the whole launch as one slice
+        p.slice_begin = 0;
+        p.slice_rows = p.n_rows;
+    }
+    if (p.wf_base && max_depth >= 2 && p.n_views == 1 && p.spp == 0) return launch_wavefront(p, max_depth, stream);
+    p.wf_base = nullptr;
     switch (max_depth) {
         case 0: return launch_depth<0>(p, stream);
         case 1: return launch_depth<1>(p, stream);
@@ -1801,7 +2074,9 @@ hipError_t allow_large_lds(size_t bytes) {
 #define RT_KFN(d) reinterpret_cast<const void *>(&render_kernel<d, false>), \
                   reinterpret_cast<const void *>(&render_kernel<d, true>)
     const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
-                         RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9)};
+                         RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9),
+                         reinterpret_cast<const void *>(&render_kernel<2, false, true>),
+                         reinterpret_cast<const void *>(&wf_trace_kernel)};
 #undef RT_KFN
     for (const void *f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));

@@ -26,7 +26,10 @@ builds = sys.argv[2:]
 ROUNDS = 7
 
 
-def load(name):
+def load(spec):
+    # BUILD[:OPTION=VALUE...]: context options (rt_context_set) after the
+    # build name, e.g. main:5=0 (RT_OPT_WAVEFRONT off)
+    name, *opts = spec.split(":")
     path = rt.LIB_PATH if name == "main" else os.path.join(ROOT, "_ab", name, "libopenglraytracer_amd.so")
     L = C.CDLL(path)
     vp, i = C.c_void_p, C.c_int
@@ -39,6 +42,9 @@ def load(name):
     ctx = C.c_void_p()
     assert L.rt_create(0, C.byref(ctx)) == 0
     L.rt_context_set(ctx, rt.abi.RT_OPT_TIMING, 0)
+    for o in opts:
+        k, v = o.split("=")
+        assert L.rt_context_set(ctx, int(k), int(v)) == 0, spec
     return L, ctx
 
 
