@@ -1499,34 +1499,35 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
 //    children's final values into its own, bottom-up; level 0 stores the pixel.
 // Same device functions, same operations per node: bit-identical to
 // trace_tree (tests/test_gpu_parity.py renders both).
-// Nodes and rays are 32-B records in the context's work buffer
-// (rt_internal.h wf_buffer_bytes); counters: per level and kind the number
-// of rays / nodes (ints 2L + kind), per level the queue head (int 32 + L).
+// Nodes and rays are 32-B records in the context's work buffer, in
+// kWfShards shards per level and kind (rt_internal.h wf_offset): a wave
+// appends the nodes / children of its chunk to shard `chunk % 64`, and a
+// launch over a level maps its chunks of 64 onto the shards' counts with a
+// wave-wide prefix sum (one shard per lane) — no counter sees more than 1/64
+// of the appends, and no launch has a global head (static chunk
+// distribution: wave g takes chunks g, g + waves, ...).
 struct WfRay {
     float4 o, d;  // start, direction (w unused)
 };
 struct WfNode {
     float4 col;  // xyz: the node's value (phong, black on a miss; mixed in place), w: meta bits
-    int4 link;   // reflection child, refraction child (-1: none), level 0: the pixel's output index
+    int4 link;   // reflection child, refraction child (slots at level + 1; -1: none), level 0: output index
 };
 constexpr uint32_t kWfSr = 1u << 8, kWfSt = 1u << 9;  // meta: material | spawned children
-__device__ __forceinline__ int *wf_counters(const LaunchParams &p) { return static_cast<int *>(p.wf_base); }
-__device__ __forceinline__ char *wf_level_base(const LaunchParams &p, int level) {
-    const size_t P = static_cast<size_t>(p.wf_cap);
-    return static_cast<char *>(p.wf_base) + kWfCounters + kWfRecord * P +
-           4 * kWfRecord * P * ((size_t{1} << (level - 1)) - 1);
+static_assert(kWfShards == 64, "one shard per lane of a wave");
+__device__ __forceinline__ int *wf_counter(const LaunchParams &p, int level, int kind, int shard) {
+    return reinterpret_cast<int *>(static_cast<char *>(p.wf_base) +
+                                   ((level * 2 + kind) * kWfShards + shard) * kWfCounterStride);
 }
 __device__ __forceinline__ WfRay *wf_rays(const LaunchParams &p, int level, int kind) {
-    const size_t cap = static_cast<size_t>(p.wf_cap) << (level - 1);
-    return reinterpret_cast<WfRay *>(wf_level_base(p, level) + kind * kWfRecord * cap);
+    return reinterpret_cast<WfRay *>(static_cast<char *>(p.wf_base) + wf_offset(p.wf_cap, level, kind));
 }
 __device__ __forceinline__ WfNode *wf_nodes(const LaunchParams &p, int level, int kind) {
-    if (level == 0) return reinterpret_cast<WfNode *>(static_cast<char *>(p.wf_base) + kWfCounters);
-    const size_t cap = static_cast<size_t>(p.wf_cap) << (level - 1);
-    return reinterpret_cast<WfNode *>(wf_level_base(p, level) + (2 + kind) * kWfRecord * cap);
+    return reinterpret_cast<WfNode *>(static_cast<char *>(p.wf_base) + wf_offset(p.wf_cap, level, level ? 2 + kind : 0));
 }
-// Wave-aggregated append (all lanes active): one atomic per wave; the lanes
-// with `want` get consecutive slots in lane order, the others -1.
+// Wave-aggregated append (the calling lanes are those with `want`... all
+// lanes active): one atomic per wave; the lanes with `want` get consecutive
+// slots in lane order, the others -1.
 __device__ __forceinline__ int wave_append(int *counter, bool want) {
     const uint64_t m = __ballot(want);
     if (!m) return -1;
@@ -1536,13 +1537,60 @@ __device__ __forceinline__ int wave_append(int *counter, bool want) {
     base = __builtin_amdgcn_readlane(base, lead);
     return want ? base + static_cast<int>(__popcll(m & ((uint64_t{1} << lane) - 1u))) : -1;
 }
+// Inclusive prefix sum over the 64 lanes (all active).
+__device__ __forceinline__ int wave_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+// A level's chunks of 64 records: reflection shards 0..63, then refraction
+// shards 0..63 (level 0: its nodes, kind 0 only); chunk c -> (kind, shard,
+// first record slot, records in the chunk).
+struct WfChunks {
+    int n_r, n_t;        // this lane's shard: records of each kind
+    int scan_r, scan_t;  // inclusive prefix sums of the shards' chunk counts
+    int total_r, total;  // chunks of kind 0, of both kinds
+    int64_t cap;         // shard capacity of the level
+};
+__device__ __forceinline__ WfChunks wf_chunks(const LaunchParams &p, int level) {
+    const int lane = threadIdx.x & 63;
+    WfChunks q;
+    q.n_r = *wf_counter(p, level, 0, lane);
+    q.n_t = level > 0 ? *wf_counter(p, level, 1, lane) : 0;
+    q.scan_r = wave_scan((q.n_r + 63) / 64);
+    q.scan_t = wave_scan((q.n_t + 63) / 64);
+    q.total_r = __builtin_amdgcn_readlane(q.scan_r, 63);
+    q.total = q.total_r + __builtin_amdgcn_readlane(q.scan_t, 63);
+    q.cap = wf_shard_cap(p.wf_cap, level);
+    return q;
+}
+// chunk c (wave-uniform, < q.total): kind, this lane's record slot, and
+// whether the lane has a record
+__device__ __forceinline__ void wf_chunk(const WfChunks &q, int c, int &kind, int &slot, bool &valid) {
+    const int lane = threadIdx.x & 63;
+    kind = c < q.total_r ? 0 : 1;
+    const int cc = kind ? c - q.total_r : c;
+    const int scan = kind ? q.scan_t : q.scan_r;
+    const int shard = static_cast<int>(__popcll(__ballot(scan <= cc)));  // shards wholly before chunk cc
+    const int before = shard ? __builtin_amdgcn_readlane(scan, shard - 1) : 0;
+    const int n = __builtin_amdgcn_readlane(kind ? q.n_t : q.n_r, shard);
+    const int i = (cc - before) * 64 + lane;
+    valid = i < n;
+    slot = static_cast<int>(shard * q.cap) + i;
+}
 // Push the children of this lane's node at `level` to level + 1 (the rays
 // trace_tree would start: :979-1030) and return their slots.
-__device__ __forceinline__ void wf_children(const LaunchParams &p, const Scene &S, int level, const Ray &ray,
-                                            const Collision &c, bool sr, bool st, int &cr, int &ct) {
-    int *cnt = wf_counters(p);
-    cr = wave_append(cnt + 2 * (level + 1), sr);
-    ct = wave_append(cnt + 2 * (level + 1) + 1, st);
+__device__ __forceinline__ void wf_children(const LaunchParams &p, const Scene &S, int level, int shard,
+                                            const Ray &ray, const Collision &c, bool sr, bool st, int &cr, int &ct) {
+    const int cap = static_cast<int>(wf_shard_cap(p.wf_cap, level + 1));
+    cr = wave_append(wf_counter(p, level + 1, 0, shard), sr);
+    ct = wave_append(wf_counter(p, level + 1, 1, shard), st);
+    if (sr) cr += shard * cap;
+    if (st) ct += shard * cap;
     if (sr) {
         const v3 o = add(c.p, muls(c.n, 0.001f)), d = reflect(ray.dir, c.n);
         wf_rays(p, level + 1, 0)[cr] = {make_float4(o.x, o.y, o.z, 0.0f), make_float4(d.x, d.y, d.z, 0.0f)};
@@ -1559,8 +1607,8 @@ __device__ __forceinline__ void wf_children(const LaunchParams &p, const Scene &
 // child at level 0 (its pixel is final); `node(value, meta, cr, ct)`: every
 // other lane with a ray (level 0: those that spawn).
 template <bool kPrimary, class Store, class Node>
-__device__ __forceinline__ void wf_trace(const LaunchParams &p, const Scene &S, int level, const Ray &ray, bool valid,
-                                         Store &&store, Node &&node) {
+__device__ __forceinline__ void wf_trace(const LaunchParams &p, const Scene &S, int level, int shard, const Ray &ray,
+                                         bool valid, Store &&store, Node &&node) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
     const Hit h = closest<kPrimary>(S, ray, valid);
     const bool hit = valid && h.obj >= 0;
@@ -1577,7 +1625,7 @@ __device__ __forceinline__ void wf_trace(const LaunchParams &p, const Scene &S, 
     }
     const v3 value = hit ? col : black;  // a missed ray is black (:962-963)
     int cr = -1, ct = -1;
-    if (__any(sr || st)) wf_children(p, S, level, ray, c, sr, st, cr, ct);
+    if (__any(sr || st)) wf_children(p, S, level, shard, ray, c, sr, st, cr, ct);
     const uint32_t meta = static_cast<uint32_t>(c.material) | (sr ? kWfSr : 0u) | (st ? kWfSt : 0u);
     if (kPrimary && valid && !(sr || st)) store(value);
     if (valid && (!kPrimary || sr || st)) node(value, meta, cr, ct);
@@ -1618,10 +1666,12 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         if constexpr (kWf) {
             // level 0 of a wavefront frame: pixels without children stored,
             // the others become level-0 nodes (their output index kept)
+            const int shard = (wy * ((p.width + 7) / 8) + wx) % kWfShards;  // the wave tile's shard
             wf_trace<true>(
-                p, S, 0, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); },
+                p, S, 0, shard, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); },
                 [&](v3 col, uint32_t meta, int cr, int ct) {
-                    const int n = wave_append(wf_counters(p), true);
+                    const int n = wave_append(wf_counter(p, 0, 0, shard), true) +
+                                  shard * static_cast<int>(wf_shard_cap(p.wf_cap, 0));
                     wf_nodes(p, 0, 0)[n] = {make_float4(col.x, col.y, col.z, __uint_as_float(meta)),
                                             make_int4(cr, ct, static_cast<int>(idx), 0)};
                 });
@@ -1809,13 +1859,14 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
 #endif
 // Levels 1..D of a wavefront frame (see wf_trace): a grid of resident
 // work-groups, each staging the scene blob into LDS once; every wave then
-// takes 64-ray chunks of the level's queues (reflection rays, then
-// refraction rays) from the level's head counter until both are drained.
+// traces 64-ray chunks of the level's queues (reflection rays, then
+// refraction rays; wf_chunks), chunks g, g + waves, ... of the level.
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WPE_WF))) void wf_trace_kernel(
     LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     const float4 *blob = static_cast<const float4 *>(p.scene);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    [[maybe_unused]] const int lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < p.blob_units; i += kThreads) lds[i] = blob[i];
 #ifdef RT_STATS
     if (lane < kStats) rt_stats_lds[wave][lane] = 0u;
@@ -1854,32 +1905,24 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WPE
     S.cull = p.view[0].cull;
     S.tx0 = S.tx1 = S.ty0 = S.ty1 = 0;
     const int level = p.wf_level;
-    int *cnt = wf_counters(p);
-    const int n_r = __builtin_amdgcn_readfirstlane(cnt[2 * level]), n_t = __builtin_amdgcn_readfirstlane(cnt[2 * level + 1]);
-    const int chunks_r = (n_r + 63) / 64, chunks = chunks_r + (n_t + 63) / 64;
-    int *head = cnt + 32 + level;
-    int chunk = 0;
-    if (lane == 0) chunk = atomicAdd(head, 1);
-    chunk = __builtin_amdgcn_readfirstlane(chunk);
-    while (chunk < chunks) {
-        int nxt = 0;
-        if (lane == 0) nxt = atomicAdd(head, 1);  // fetched one chunk ahead
-        const int kind = chunk < chunks_r ? 0 : 1;
-        const int i = (chunk - (kind ? chunks_r : 0)) * 64 + lane;
-        const bool valid = i < (kind ? n_t : n_r);
+    const WfChunks q = wf_chunks(p, level);
+    const int n_waves = static_cast<int>(gridDim.x) * (kThreads / 64);
+    for (int c = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave; c < q.total; c += n_waves) {
+        int kind, slot;
+        bool valid;
+        wf_chunk(q, c, kind, slot, valid);
         Ray ray{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 1.0f)};
         if (valid) {
-            const WfRay r = wf_rays(p, level, kind)[i];
+            const WfRay r = wf_rays(p, level, kind)[slot];
             ray.start = mk(r.o.x, r.o.y, r.o.z);
             ray.dir = mk(r.d.x, r.d.y, r.d.z);
         }
         WfNode *nodes = wf_nodes(p, level, kind);
         wf_trace<false>(
-            p, S, level, ray, valid, [](v3) {},
+            p, S, level, c % kWfShards, ray, valid, [](v3) {},
             [&](v3 col, uint32_t meta, int cr, int ct) {
-                nodes[i] = {make_float4(col.x, col.y, col.z, __uint_as_float(meta)), make_int4(cr, ct, 0, 0)};
+                nodes[slot] = {make_float4(col.x, col.y, col.z, __uint_as_float(meta)), make_int4(cr, ct, 0, 0)};
             });
-        chunk = __builtin_amdgcn_readfirstlane(nxt);
     }
 #ifdef RT_STATS
     if (lane < kStats) atomicAdd(&rt_stats[lane], static_cast<unsigned long long>(rt_stats_lds[wave][lane]));
@@ -1898,15 +1941,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WPE
 __global__ __launch_bounds__(kThreads) void wf_mix_kernel(LaunchParams p) {
     const int level = p.wf_level;
     const MatRec *mat = reinterpret_cast<const MatRec *>(static_cast<const float4 *>(p.scene) + p.off_mats);
-    const int *cnt = wf_counters(p);
-    const int n0 = cnt[2 * level], n1 = level == 0 ? 0 : cnt[2 * level + 1];
-    const int stride = static_cast<int>(gridDim.x) * kThreads;
-    for (int g = static_cast<int>(blockIdx.x) * kThreads + static_cast<int>(threadIdx.x); g < n0 + n1; g += stride) {
-        const int kind = g < n0 ? 0 : 1, i = kind ? g - n0 : g;
+    const WfChunks q = wf_chunks(p, level);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int n_waves = static_cast<int>(gridDim.x) * (kThreads / 64);
+    for (int c = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave; c < q.total; c += n_waves) {
+        int kind, slot;
+        bool valid;
+        wf_chunk(q, c, kind, slot, valid);
+        if (!valid) continue;
         WfNode *nodes = wf_nodes(p, level, kind);
-        const WfNode nd = nodes[i];
+        const WfNode nd = nodes[slot];
         const uint32_t meta = __float_as_uint(nd.col.w);
-        if (!(meta & (kWfSr | kWfSt))) continue;
+        if (!(meta & (kWfSr | kWfSt))) continue;  // a leaf: its value is final
         const MatRec &m = mat[meta & 0xFFu];
         v3 value = mk(nd.col.x, nd.col.y, nd.col.z);
         if (meta & kWfSr) {
@@ -1920,7 +1966,7 @@ __global__ __launch_bounds__(kThreads) void wf_mix_kernel(LaunchParams p) {
         if (level == 0)
             store_pixel(p, 0, static_cast<uint32_t>(nd.link.z), value);
         else
-            nodes[i].col = make_float4(value.x, value.y, value.z, nd.col.w);
+            nodes[slot].col = make_float4(value.x, value.y, value.z, nd.col.w);
     }
 }
 
@@ -1969,17 +2015,19 @@ hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
 // work buffer (p.wf_cap pixels), the counters cleared, level 0, levels 1..D,
 // then the mixes D-1..0 — all queued on `stream`.
 hipError_t launch_wavefront(LaunchParams &p, int depth, hipStream_t stream) {
-    const int slice_rows = std::max(8, p.wf_cap / p.width / 8 * 8);
+    const int slice_rows = std::max(8, p.wf_cap / ((p.width + 7) / 8 * 8) / 8 * 8);
     const size_t lds0 = lds_bytes(p), lds1 = static_cast<size_t>(p.blob_units) * sizeof(float4);
     const void *trace_fn = reinterpret_cast<const void *>(&wf_trace_kernel);
     const int resident = std::max(1, groups_per_cu(trace_fn, lds1) * std::max(p.n_cu, 1));
-    const int mix_groups = std::max(1, 8 * std::max(p.n_cu, 1));
+    const int mix_groups = std::max(1, 4 * std::max(p.n_cu, 1));
     p.sched = nullptr;
     p.wf_level = 0;
     for (int begin = 0; begin < p.n_rows; begin += slice_rows) {
         p.slice_begin = begin;
         p.slice_rows = std::min(slice_rows, p.n_rows - begin);
-        hipError_t e = hipMemsetAsync(p.wf_base, 0, kWfCounters, stream);
+        // the counters of levels 0..depth
+        hipError_t e = hipMemsetAsync(p.wf_base, 0, static_cast<size_t>(depth + 1) * 2 * kWfShards * kWfCounterStride,
+                                      stream);
         if (e != hipSuccess) return e;
         const dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, 1);
         hipLaunchKernelGGL((render_kernel<2, false, true>), grid, dim3(kThreads), lds0, stream, p);
