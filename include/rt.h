@@ -298,12 +298,13 @@ int rt_multi_last_ms(rt_multi *m, float *kernel_ms, float *gather_ms, float *ass
  * 16 spheres + 1 box);
  * 0: every work-group derives them on the device. Output is identical. */
 #define RT_OPT_FRAME_CONSTS 4
-/* RT_OPT_WAVEFRONT (default 1): frames of max_depth >= 2 (one view, no
- * Monte-Carlo accumulation) are rendered level by level — the camera rays,
- * then every bounce level's reflection and refraction rays from queues, then
- * the colour mixes bottom-up — instead of one depth-first walk per pixel;
- * the context keeps a device work buffer for it (at most 8 GiB; larger frames
- * run in row slices). 0: the depth-first walk. Output is identical. */
+/* RT_OPT_WAVEFRONT (default 0): 1 renders frames of max_depth >= 2 (one
+ * view, no Monte-Carlo accumulation) level by level — the camera rays, then
+ * every bounce level's reflection and refraction rays from queues, then the
+ * colour mixes bottom-up — instead of one depth-first walk per pixel; the
+ * context then keeps a device work buffer for it (at most 8 GiB; larger
+ * frames run in row slices). Output is identical; the depth-first walk (0)
+ * measured about 2x faster on configs 3 and 4. */
 #define RT_OPT_WAVEFRONT 5
 int rt_context_set(rt_context *ctx, int option, int value);
 

@@ -224,7 +224,8 @@ class Context:
 
     def set_wavefront(self, on):
         """RT_OPT_WAVEFRONT: depth >= 2 frames level by level from ray queues
-        (default) instead of the per-pixel depth-first walk (output identical)."""
+        instead of the per-pixel depth-first walk (the default; output
+        identical; the walk measured 2x faster)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_WAVEFRONT, 1 if on else 0))
 
     def set_output(self, fmt):

@@ -298,7 +298,7 @@ struct rt_context {
     int timing = 1;   // RT_OPT_TIMING
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int host_consts = 1;  // RT_OPT_FRAME_CONSTS
-    int wavefront = 1;    // RT_OPT_WAVEFRONT: depth >= 2 frames level by level (rt_kernel.hip)
+    int wavefront = 0;    // RT_OPT_WAVEFRONT: depth >= 2 frames level by level (rt_kernel.hip)
     void *wf_buf = nullptr;  // its work buffer (grown on demand)
     size_t wf_bytes = 0;
     hipEvent_t wf_done = nullptr;  // recorded after the last wavefront render (launches on other streams wait)

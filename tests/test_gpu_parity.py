@@ -850,8 +850,8 @@ def test_stratified_crops_product_path_matches_gl(gpu_ctx, name):
 
 # ---- wavefront path (RT_OPT_WAVEFRONT, rt_kernel.hip wf_*) -----------------
 def render_both_walks(ctx, objs, w, h, depth, view, rows=None, shard=None):
-    """The same frame through the level-by-level wavefront path (default)
-    and through the per-pixel depth-first walk."""
+    """The same frame through the level-by-level wavefront path and through
+    the per-pixel depth-first walk (the default)."""
     sc = rt.Scene(ctx, objs)
     out = []
     try:
@@ -866,7 +866,7 @@ def render_both_walks(ctx, objs, w, h, depth, view, rows=None, shard=None):
                 torch.cuda.synchronize()
                 out.append(buf.cpu().numpy().reshape(-1, w, 4))
     finally:
-        ctx.set_wavefront(True)
+        ctx.set_wavefront(False)
         sc.close()
     return out
 
@@ -934,5 +934,5 @@ def test_wavefront_config4_full_frame_slices_equal_walk(gpu_ctx):
             outs.append(out)
         assert torch.equal(outs[0], outs[1])
     finally:
-        gpu_ctx.set_wavefront(True)
+        gpu_ctx.set_wavefront(False)
         sc.close()
