@@ -723,7 +723,7 @@ __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int b
 // walk (config 2 even).
 // p = the shaded point, L = the light. Called with all lanes active.
 __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
-                                              uint64_t mask, bool need) {
+                                              uint64_t mask, bool need, const uint4 *pre) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     RT_STAT(7, need);
@@ -815,7 +815,11 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
             // 16.63 -> 14.83 ms, config 3 0.940 -> 0.896 ms, r03c; the
             // wave's candidate passes per tile 68.8 -> 52.5)
             uint4 rec = make_uint4(0u, 0u, 0u, 0u);
-            if (need && !hit && texel >= 0) rec = S.glist[static_cast<size_t>(slot) * per_light + texel];
+            if (pre) {
+                if (need && !hit && texel >= 0) rec = *pre;
+            } else if (need && !hit && texel >= 0) {
+                rec = S.glist[static_cast<size_t>(slot) * per_light + texel];
+            }
             uint32_t cnt = rec.x & 0xFFu;
             const bool wide = need && !hit && (texel < 0 || cnt == kGListOverflow);
             if (wide) cnt = 0u;
@@ -978,9 +982,9 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
 }
 
 __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
-                                         uint64_t mask, bool need) {
+                                         uint64_t mask, bool need, const uint4 *pre = nullptr) {
     RT_CYC(kCycShadow);
-    const bool hit = occluded_impl(S, start, dir, p, L, light, slot, mask, need);
+    const bool hit = occluded_impl(S, start, dir, p, L, light, slot, mask, need, pre);
     RT_CYC_AFTER(kCycPhong, hit ? 1 : 0);
     return hit;
 }
@@ -1079,6 +1083,16 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
         ++slot;
         const v3 lpos = mk(L.pos[0], L.pos[1], L.pos[2]);
         const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
+#ifdef RT_SHADOW_PREFETCH
+        // the texel's candidate list requested before the shading math, for
+        // every lane with a hit (its latency overlaps the math)
+        int ptexel = -1;
+        uint4 pre = make_uint4(0u, 0u, 0u, 0u);
+        if (S.glist) {
+            ptexel = valid ? direction_texel(kGMaskTexels, muls(sdir, -1.0f)) : -1;
+            if (ptexel >= 0) pre = S.glist[static_cast<size_t>(slot) * 6 * kGMaskTexels * kGMaskTexels + ptexel];
+        }
+#endif
         const v3 ldir = normalize(sdir);
         const float cos_theta = dot(ldir, c.n);
         // reflect(-ldir, n) needs dot(n, -ldir), which is -cos_theta (exact
@@ -1123,12 +1137,22 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
             // mask of a lane without the query): no divergent branch around
             // the lookup (config 2 -1 %); the wide-mask texel only where the
             // query is cast (unguarded, config 3 +0.7 %)
+#ifdef RT_SHADOW_PREFETCH
+            if (S.glist)
+                smask = static_cast<uint64_t>(static_cast<int64_t>(ptexel));
+            else
+#endif
             if (S.gmask && need)  // wide masks win where both exist (as in occluded)
                 smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
             else if (S.dmask && !S.gmask)
                 smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
                                        S.dmask_bytes, muls(sdir, -1.0f), S.ns);
+#ifdef RT_SHADOW_PREFETCH
+            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need,
+                                           S.glist ? &pre : nullptr);
+#else
             const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need);
+#endif
             if (need && !shadowed) {
                 dif = nd;
                 spe = ns;
