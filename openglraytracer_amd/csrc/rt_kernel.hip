@@ -1083,16 +1083,15 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
         ++slot;
         const v3 lpos = mk(L.pos[0], L.pos[1], L.pos[2]);
         const v3 sdir = sub(lpos, c.p);  // the shadow ray's direction (:809)
-#ifdef RT_SHADOW_PREFETCH
-        // the texel's candidate list requested before the shading math, for
-        // every lane with a hit (its latency overlaps the math)
+        // wide masks: the texel's candidate list requested before the shading
+        // math, for every lane with a hit, so its L2 latency overlaps the
+        // math (config 4 14.92 -> 14.77 ms, config 3 0.893 -> 0.889 ms, r03b)
         int ptexel = -1;
         uint4 pre = make_uint4(0u, 0u, 0u, 0u);
         if (S.glist) {
             ptexel = valid ? direction_texel(kGMaskTexels, muls(sdir, -1.0f)) : -1;
             if (ptexel >= 0) pre = S.glist[static_cast<size_t>(slot) * 6 * kGMaskTexels * kGMaskTexels + ptexel];
         }
-#endif
         const v3 ldir = normalize(sdir);
         const float cos_theta = dot(ldir, c.n);
         // reflect(-ldir, n) needs dot(n, -ldir), which is -cos_theta (exact
@@ -1137,22 +1136,15 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
             // mask of a lane without the query): no divergent branch around
             // the lookup (config 2 -1 %); the wide-mask texel only where the
             // query is cast (unguarded, config 3 +0.7 %)
-#ifdef RT_SHADOW_PREFETCH
             if (S.glist)
                 smask = static_cast<uint64_t>(static_cast<int64_t>(ptexel));
-            else
-#endif
-            if (S.gmask && need)  // wide masks win where both exist (as in occluded)
+            else if (S.gmask && need)  // wide masks win where both exist (as in occluded)
                 smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
             else if (S.dmask && !S.gmask)
                 smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
                                        S.dmask_bytes, muls(sdir, -1.0f), S.ns);
-#ifdef RT_SHADOW_PREFETCH
             const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need,
                                            S.glist ? &pre : nullptr);
-#else
-            const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need);
-#endif
             if (need && !shadowed) {
                 dif = nd;
                 spe = ns;
@@ -1388,7 +1380,10 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #ifndef RT_WPE_DEEP
 #define RT_WPE_DEEP 6
 #endif
-#define RT_WAVES_PER_EU(d) ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1))
+#ifndef RT_WPE2
+#define RT_WPE2 7  // depth 2 (config 3): 7 waves 0.878 vs 6 waves 0.893 ms; depth 4: 6 waves 14.92 vs 7 15.21 ms (r03b)
+#endif
+#define RT_WAVES_PER_EU(d) ((d) == 2 ? RT_WPE2 : ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1)))
 #endif
 #define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(kDepth))))
 // Reductions over aligned groups of 8 lanes (DPP: quad butterflies, then the

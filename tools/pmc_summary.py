@@ -134,7 +134,7 @@ if out["l2_hit_per_launch"] is not None and out["l2_miss_per_launch"] is not Non
     tot = out["l2_hit_per_launch"] + out["l2_miss_per_launch"]
     out["l2_hit_rate"] = out["l2_hit_per_launch"] / tot if tot else None
 allc = {}
-for name in ("pmc_write", "pmc_fetch", "pmc_sq", "pmc_cyc", "pmc_l2"):
+for name in ("pmc_write", "pmc_fetch", "pmc_sq", "pmc_cyc", "pmc_l2", "pmc_lds"):
     for cname, vals in counters(name).items():
         allc[cname] = per_launch(vals)
 out["counters_per_launch"] = allc
