@@ -1277,8 +1277,15 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
             Frame fr;
             fr.col = col;
             fr.rs = sub(c.p, muls(c.n, 0.001f));
-            const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
-            fr.rd = refract(ray.dir, c.n, ratio);
+            fr.rd = ray.dir;  // (no refraction child: never read)
+#ifndef RT_EAGER_REFRACT
+            if (__any(st)) {  // only waves with a refraction child (every surface reflects, few refract)
+#else
+            {
+#endif
+                const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
+                fr.rd = refract(ray.dir, c.n, ratio);
+            }
             fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3);
             F.set(level, fr);
             if (sr) {
@@ -1381,7 +1388,10 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #define RT_WPE_DEEP 6
 #endif
 #ifndef RT_WPE2
-#define RT_WPE2 7  // depth 2 (config 3): 7 waves 0.878 vs 6 waves 0.893 ms; depth 4: 6 waves 14.92 vs 7 15.21 ms (r03b)
+// depth 2 (config 3): 7 waves timed 0.878 vs 0.893 ms in short bursts (r03b),
+// but raised the HBM traffic 2.4 -> 4.1 GB per frame (216 B of scratch per
+// lane) and the sustained bench kernel to 1.03 ms at a 1.99 GHz clock (r03c)
+#define RT_WPE2 6
 #endif
 #define RT_WAVES_PER_EU(d) ((d) == 2 ? RT_WPE2 : ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1)))
 #endif
