@@ -26,7 +26,7 @@ struct SphereMeta {
     int32_t obj_index;
     int32_t material;
     float radius;  // |radius|, for the culling bounds (intersection uses rr)
-    int32_t tame;  // 1: finite, |centre| <= 1e3, |radius| in [1e-3, 1e3] (own-sphere shadow skip)
+    int32_t pad;
 };
 
 // One oriented box (:647-724) with its frame constants precomputed once per

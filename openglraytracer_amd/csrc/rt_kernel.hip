@@ -723,7 +723,7 @@ __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int b
 // walk (config 2 even).
 // p = the shaded point, L = the light. Called with all lanes active.
 __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
-                                              uint64_t mask, bool need, const uint4 *pre, int own) {
+                                              uint64_t mask, bool need, const uint4 *pre) {
     bool hit = false;
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     RT_STAT(7, need);
@@ -823,34 +823,6 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
             uint32_t cnt = rec.x & 0xFFu;
             const bool wide = need && !hit && (texel < 0 || cnt == kGListOverflow);
             if (wide) cnt = 0u;
-#ifdef RT_SKIP_OWN
-            // the lane's own sphere (own >= 0: hit from outside, light in
-            // front, tame) provably cannot block the segment: the list is
-            // walked without it, so a lane needs one pass fewer when it is
-            // listed (each lane keeps its own position k in its list)
-            const auto entry = [&](uint32_t k) {
-                const uint32_t word = k < 4 ? rec.x : (k < 8 ? rec.y : (k < 12 ? rec.z : rec.w));
-                return (word >> (8 * (k & 3u))) & 0xFFu;
-            };
-            const uint32_t self = own >= 0 ? static_cast<uint32_t>(own) : 0x100u;
-            uint32_t k = 1u, cur = 0u;
-            if (k <= cnt) {
-                cur = entry(k);
-                if (cur == self && ++k <= cnt) cur = entry(k);
-            }
-            while (__any(k <= cnt)) {
-                RT_STAT(9, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
-                if (k <= cnt) {
-                    exact_cand(static_cast<int>(cur));
-                    if (hit) cnt = 0u;
-                    if (++k <= cnt) {
-                        cur = entry(k);
-                        if (cur == self && ++k <= cnt) cur = entry(k);
-                    }
-                }
-            }
-#else
-            (void)own;
             for (uint32_t i = 1; __any(i <= cnt); ++i) {  // i: wave-uniform
                 RT_STAT(9, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (i <= cnt) {
@@ -859,7 +831,6 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
                     if (hit) cnt = 0u;
                 }
             }
-#endif
             if (!__any(wide)) return hit;
             ask = wide;  // more than kGListMax candidates, or every sphere: the words
         }
@@ -1011,9 +982,9 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
 }
 
 __device__ __forceinline__ bool occluded(const Scene &S, v3 start, v3 dir, v3 p, v3 L, int light, int slot,
-                                         uint64_t mask, bool need, const uint4 *pre = nullptr, int own = -1) {
+                                         uint64_t mask, bool need, const uint4 *pre = nullptr) {
     RT_CYC(kCycShadow);
-    const bool hit = occluded_impl(S, start, dir, p, L, light, slot, mask, need, pre, own);
+    const bool hit = occluded_impl(S, start, dir, p, L, light, slot, mask, need, pre);
     RT_CYC_AFTER(kCycPhong, hit ? 1 : 0);
     return hit;
 }
@@ -1022,9 +993,6 @@ struct Collision {
     v3 p, n;
     bool inside;
     int material;
-#ifdef RT_SKIP_OWN
-    int own;  // the hit sphere's slot when hit from outside and tame (rt_scene.cpp), else -1
-#endif
 };
 
 // Build the collision record of the winning object (:628-637, :686-721).
@@ -1037,18 +1005,11 @@ __device__ __forceinline__ Collision resolve_impl(const Scene &S, const Ray &r, 
     c.n = mk(0.0f, 0.0f, 1.0f);
     c.inside = false;
     c.material = 0;
-#ifdef RT_SKIP_OWN
-    c.own = -1;
-#endif
     if (!valid) return c;
     if (h.slot >= 0) {
         const float4 sp = S.sph[h.slot];
         const v3 pos = mk(sp.x, sp.y, sp.z);
-        const int4 meta = S.smeta[h.slot];
-        c.material = meta.y;
-#ifdef RT_SKIP_OWN
-        c.own = (meta.w != 0 && !(h.info & 1)) ? h.slot : -1;
-#endif
+        c.material = S.smeta[h.slot].y;
         c.p = add(r.start, muls(r.dir, h.t));
         c.n = normalize(sub(c.p, pos));
         c.inside = h.info & 1;
@@ -1182,13 +1143,8 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
             else if (S.dmask && !S.gmask)
                 smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
                                        S.dmask_bytes, muls(sdir, -1.0f), S.ns);
-#ifdef RT_SKIP_OWN
-            const int own = cos_theta > 0.0f ? c.own : -1;
-#else
-            const int own = -1;
-#endif
             const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need,
-                                           S.glist ? &pre : nullptr, own);
+                                           S.glist ? &pre : nullptr);
             if (need && !shadowed) {
                 dif = nd;
                 spe = ns;
@@ -1823,6 +1779,24 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
             rt_phase_buf[wg_ * 16 + 8] = hw;
             rt_phase_buf[wg_ * 16 + 9] = xcc;
         }
+    }
+#endif
+#ifndef RT_LAZY_ARGS
+    // The kernel arguments the prologue branches on or computes with, loaded
+    // in one batch and waited for once (the asm wants them in SGPRs here):
+    // left alone, the compiler issued the scalar loads a few at a time between
+    // the prologue's branches — about eight dependent round trips to the
+    // argument block per wave (r03d phase trace of a 1080p depth-0 frame: 2.9
+    // of the 4.3 us prologue). The view's matrix and origin go as 8-B pairs.
+    {
+        const uint64_t *vw = reinterpret_cast<const uint64_t *>(&V);  // FrameView: 8-B aligned, unproj first
+        static_assert(offsetof(FrameView, unproj) == 0 && offsetof(FrameView, origin) == 128 &&
+                          offsetof(FrameView, cull) == 140 && sizeof(FrameView) % 8 == 0,
+                      "FrameView layout (argument prefetch)");
+        asm volatile("" ::"s"(p.width), "s"(p.height), "s"(p.row_begin), "s"(p.block_rows), "s"(p.n_shards),
+                     "s"(p.shard), "s"(p.blob_units), "s"(p.n_frame_consts), "s"(p.slice_begin), "s"(p.slice_rows),
+                     "s"(V.blob), "s"(p.scene), "s"(vw[0]), "s"(vw[1]), "s"(vw[2]), "s"(vw[3]), "s"(vw[4]),
+                     "s"(vw[5]), "s"(vw[6]), "s"(vw[7]), "s"(vw[16]), "s"(vw[17]));
     }
 #endif
     const float4 *blob = static_cast<const float4 *>(V.blob ? V.blob : p.scene);

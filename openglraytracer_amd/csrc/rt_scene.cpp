@@ -760,16 +760,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
             sph.push_back({o.position[0], o.position[1], o.position[2], o.radius * o.radius});
             // |radius| for the culling bounds (a negative radius other than -1
             // is a sphere of radius |r|: the test only sees r*r, :588)
-            // pad = 1: a "tame" sphere (finite, |centre| <= 1e3, |radius| in
-            // [1e-3, 1e3]), for which a shadow ray from its own outside surface
-            // towards a light in front of it provably misses it (rt_kernel.hip
-            // occluded_impl): float error stays far below the 0.01 start offset
-            const float ar = std::fabs(o.radius);
-            const bool tame = std::isfinite(o.position[0]) && std::isfinite(o.position[1]) &&
-                              std::isfinite(o.position[2]) && std::fabs(o.position[0]) <= 1e3f &&
-                              std::fabs(o.position[1]) <= 1e3f && std::fabs(o.position[2]) <= 1e3f &&
-                              ar >= 1e-3f && ar <= 1e3f;
-            smeta.push_back({i, o.material, ar, tame ? 1 : 0});
+            smeta.push_back({i, o.material, std::fabs(o.radius), 0});
         } else {
             // the transforms as the reference's GL evaluates them per ray (rt_camera.cpp)
             float L[16], W[16], N[9];
