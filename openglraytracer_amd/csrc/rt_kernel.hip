@@ -1278,11 +1278,10 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
             fr.col = col;
             fr.rs = sub(c.p, muls(c.n, 0.001f));
             fr.rd = ray.dir;  // (no refraction child: never read)
-#ifndef RT_EAGER_REFRACT
-            if (__any(st)) {  // only waves with a refraction child (every surface reflects, few refract)
-#else
-            {
-#endif
+            // only in waves with a refraction child (every surface of the
+            // bench scenes reflects, few refract: config 4 14.68 -> 14.62 ms,
+            // config 3 0.881 -> 0.878 ms, r03d)
+            if (__any(st)) {
                 const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
                 fr.rd = refract(ray.dir, c.n, ratio);
             }
@@ -1779,24 +1778,6 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
             rt_phase_buf[wg_ * 16 + 8] = hw;
             rt_phase_buf[wg_ * 16 + 9] = xcc;
         }
-    }
-#endif
-#ifndef RT_LAZY_ARGS
-    // The kernel arguments the prologue branches on or computes with, loaded
-    // in one batch and waited for once (the asm wants them in SGPRs here):
-    // left alone, the compiler issued the scalar loads a few at a time between
-    // the prologue's branches — about eight dependent round trips to the
-    // argument block per wave (r03d phase trace of a 1080p depth-0 frame: 2.9
-    // of the 4.3 us prologue). The view's matrix and origin go as 8-B pairs.
-    {
-        const uint64_t *vw = reinterpret_cast<const uint64_t *>(&V);  // FrameView: 8-B aligned, unproj first
-        static_assert(offsetof(FrameView, unproj) == 0 && offsetof(FrameView, origin) == 128 &&
-                          offsetof(FrameView, cull) == 140 && sizeof(FrameView) % 8 == 0,
-                      "FrameView layout (argument prefetch)");
-        asm volatile("" ::"s"(p.width), "s"(p.height), "s"(p.row_begin), "s"(p.block_rows), "s"(p.n_shards),
-                     "s"(p.shard), "s"(p.blob_units), "s"(p.n_frame_consts), "s"(p.slice_begin), "s"(p.slice_rows),
-                     "s"(V.blob), "s"(p.scene), "s"(vw[0]), "s"(vw[1]), "s"(vw[2]), "s"(vw[3]), "s"(vw[4]),
-                     "s"(vw[5]), "s"(vw[6]), "s"(vw[7]), "s"(vw[16]), "s"(vw[17]));
     }
 #endif
     const float4 *blob = static_cast<const float4 *>(V.blob ? V.blob : p.scene);
