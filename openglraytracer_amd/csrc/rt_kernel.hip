@@ -1201,7 +1201,8 @@ struct Frame {
     v3 rs, rd;    // pending refraction ray (:1010-1023)
     int flags;    // 1: refraction spawned; 2: waiting for the reflection; 4: for the refraction;
                   // | material << 3 (rho and tau read back from it: a 40-B frame instead of
-                  // 48, config 4 18.68 -> 18.26 ms, config 3 1.022 -> 1.000 ms)
+                  // 48, config 4 18.68 -> 18.26 ms, config 3 1.022 -> 1.000 ms; the flags
+                  // beside the colour, so a pop reads one 16-B word, measured even, r03h)
 };
 
 #ifdef RT_ABLATE_FRAMES
