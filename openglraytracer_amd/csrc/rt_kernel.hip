@@ -1395,7 +1395,11 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #endif
 #define RT_WAVES_PER_EU(d) ((d) == 2 ? RT_WPE2 : ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1)))
 #endif
-#define RT_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU(kDepth))))
+#ifndef RT_WPE0_MC
+#define RT_WPE0_MC RT_WPE0  // depth-0 Monte-Carlo kernel (config 5)
+#endif
+#define RT_OCCUPANCY \
+    __attribute__((amdgpu_waves_per_eu((kAccum && kDepth == 0) ? RT_WPE0_MC : RT_WAVES_PER_EU(kDepth))))
 // Reductions over aligned groups of 8 lanes (DPP: quad butterflies, then the
 // half-row mirror); every lane of the group ends with the result.
 __device__ __forceinline__ float group8_min(float v) {

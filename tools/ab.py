@@ -39,6 +39,7 @@ def load(spec):
     L.rt_context_set.argtypes = [vp, i, i]
     L.rt_render_view.argtypes = [vp, vp, vp, i, i, i, i, i, vp, i, vp]
     L.rt_render_batch.argtypes = [vp, vp, vp, i, i, i, i, i, i, i, vp, vp]
+    L.rt_render_accumulate.argtypes = [vp, vp, vp, i, i, i, i, i, C.c_uint32, i, i, i, vp, vp]
     ctx = C.c_void_p()
     assert L.rt_create(0, C.byref(ctx)) == 0
     L.rt_context_set(ctx, rt.abi.RT_OPT_TIMING, 0)
@@ -55,8 +56,10 @@ mats = rt.reference_materials()
 lights = rt.reference_lights()
 view = rt.make_view(None, 0.0)
 for cfg in cfgs:
-    # "<config>x<K>": K animated frames (t = k / 60) per launch (rt_render_batch)
+    # "<config>x<K>": K animated frames (t = k / 60) per launch (rt_render_batch);
+    # "config5": Monte-Carlo, 16 jittered samples per launch (rt_render_accumulate)
     batch = int(cfg.split("x")[1]) if "x" in cfg.replace("config", "") else 0
+    mc_spp = 16 if cfg == "config5" else 0
     build, w, h, depth = scenes.CONFIGS[cfg.split("x")[0]]
     views = (rt.View * max(batch, 1))(*[rt.make_view(None, k / 60.0) for k in range(max(batch, 1))])
     objs = build()
@@ -66,7 +69,7 @@ for cfg in cfgs:
     out = torch.empty((max(batch, 1), h, w, 4), dtype=torch.float32, device="cuda")
     # sustained timing: each timed block is about 60 ms of GPU work (short
     # bursts run at a higher clock than the bench's back-to-back launches)
-    est_ms = {"config1": 0.03, "config2": 0.045, "config3": 1.0, "config4": 15.0, "config5": 0.045}.get(
+    est_ms = {"config1": 0.03, "config2": 0.045, "config3": 1.0, "config4": 15.0, "config5": 0.045 * 16}.get(
         cfg.split("x")[0], 1.0) * max(batch, 1)
     reps = max(2, int(round(60.0 / est_ms)))
     state = {}
@@ -79,7 +82,10 @@ for cfg in cfgs:
 
     def launch(b):
         L, ctx = libs[b]
-        if batch:
+        if mc_spp:
+            rc = L.rt_render_accumulate(ctx, state[b], C.byref(view), w, h, depth, mc_spp, 0, 0, 1, 0, h,
+                                        C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream))
+        elif batch:
             rc = L.rt_render_batch(ctx, state[b], views, batch, w, h, depth, 8, 1, 0, C.c_void_p(out.data_ptr()),
                                    C.c_void_p(stream.cuda_stream))
         else:
@@ -88,6 +94,8 @@ for cfg in cfgs:
         assert rc == 0, rc
 
     for b in builds:  # warm-up + frame hash
+        if mc_spp:
+            out.zero_()
         launch(b)
         torch.cuda.synchronize()
         digests[b] = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
@@ -103,7 +111,7 @@ for cfg in cfgs:
             torch.cuda.synchronize()
             times[b].append(e0.elapsed_time(e1) / reps)
     for b in builds:
-        t = np.array(times[b]) / max(batch, 1)  # per frame
+        t = np.array(times[b]) / max(batch, 1, mc_spp)  # per frame (per sample)
         print("%-8s %-10s median %.4f ms  min %.4f ms  frame %s" % (cfg, b, np.median(t), t.min(), digests[b]),
               flush=True)
     for b, (L, ctx) in libs.items():
