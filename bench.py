@@ -18,10 +18,12 @@ tail). The total work of a step is fixed: strong scaling.
     all F frames (rt_render_batch with shards), one RCCL gather per step
     brings the shards to rank 0, which de-interleaves them into the F frames;
     the gather of step i overlaps the render of step i+1 (double-buffered).
-    The shards travel in the shipped app's GL_RGBA8 surface format
+    The kernel writes the shipped app's GL_RGBA8 surface format
     (main.cpp:152-159, :223; RT_OUTPUT_RGBA8, byte-exact vs the reference's
-    GL render): 4 B per pixel instead of 16 — 8.3 MB per 1080p frame through
-    rank 0's xGMI ingress. The line also carries `independent_frames`: every
+    GL render), and the shards travel without its alpha byte, which is always
+    0 (:404): 3 B per pixel instead of 16 — 6.2 MB per 1080p frame through
+    rank 0's xGMI ingress — into one contiguous buffer that a single
+    index_select de-interleaves. The line also carries `independent_frames`: every
     rank renders F whole frames of its own with no collective (weak scaling),
     and `verified`: the assembled frames of the last step equal rank 0's own
     whole-frame render byte for byte. --frame-exchange all_to_all instead
@@ -301,7 +303,27 @@ def main():
             for j, vs in chunks:
                 rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * frame_elems, W, H, DEPTH, vs,
                                 BLOCK_ROWS, world, rank, stream=sh)
-        if mode == "gather":
+        if mode == "gather" and surf == "rgba8":
+            # GL_RGBA8 shards sent without their alpha byte (always 0, :404):
+            # 3 B per pixel through rank 0's xGMI ingress instead of 4; the
+            # gather lands in one contiguous buffer per slot, and one
+            # index_select de-interleaves all F frames (packed RGB8, alpha 0)
+            px = frame.flat_shard_elems(n_frames, H, W, BLOCK_ROWS, world, 1)
+            sends = [torch.empty(px * 3, dtype=torch.uint8, device=coll_dev) for _ in bufs]
+            bigs = ([torch.empty(world * px * 3, dtype=torch.uint8, device=coll_dev) for _ in bufs]
+                    if rank == 0 else None)
+            idx = torch.as_tensor(frame.contiguous_assembly_rows(n_frames, H, BLOCK_ROWS, world), device=coll_dev)
+
+            def collective(slot, src):
+                frame.pack_rgb8(src, sends[slot])
+                dist.gather(sends[slot], [bigs[slot][r * px * 3:(r + 1) * px * 3] for r in range(world)]
+                            if rank == 0 else None, dst=0)  # RCCL: every shard to rank 0
+
+            def assemble(slot):
+                if rank == 0:
+                    return frame.assemble_contiguous(bigs[slot], n_frames, H, W, 3, idx)
+                return None
+        elif mode == "gather":
             glists = ([[torch.empty(elems, dtype=dt, device=coll_dev) for _ in range(world)] for _ in bufs]
                       if rank == 0 else None)
             perm = torch.as_tensor(frame.assembly_permutation(H, BLOCK_ROWS, world), device=coll_dev)
@@ -461,14 +483,19 @@ def main():
         mismatch count is summed over the ranks that assemble."""
         bad, px = 0, 0
         if plan.last is not None:
-            got = plan.last.reshape(n_frames, H, W, ch)
             ref = torch.zeros((n_frames, H, W, ch), dtype=dt, device="cuda")
             views = [rt.make_view(None, t) for t in times]
             for j in range(0, n_frames, rt.abi.RT_MAX_BATCH):
                 rt.render_batch(ctx, scene, ref[j].data_ptr(), W, H, DEPTH, views[j:j + rt.abi.RT_MAX_BATCH])
             torch.cuda.synchronize()
-            diff = (got.to(ref.device) != ref).reshape(n_frames * H * W, ch).any(-1)
-            bad, px = int(diff.sum().item()), n_frames * H * W
+            if plan.last.dtype == torch.uint8:  # RGB8 frames (the alpha byte dropped): against the RGBA8 texels
+                texels = ref.view(torch.uint8).reshape(n_frames, H, W, 4)
+                got = plan.last.reshape(n_frames, H, W, 3).to(ref.device)
+                diff = (got != texels[..., :3]).any(-1) | (texels[..., 3] != 0)
+            else:
+                got = plan.last.reshape(n_frames, H, W, ch)
+                diff = (got.to(ref.device) != ref).reshape(n_frames * H * W, ch).any(-1)
+            bad, px = int(diff.reshape(-1).sum().item()), n_frames * H * W
         if world > 1:
             t = torch.tensor([bad, px], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t)
@@ -555,7 +582,10 @@ def main():
         elif batched and mode == "gather":
             collective = "gather to rank 0 (one per step: the shards of all F frames)"
             workload.update({"frames_per_step": F, "frames_per_launch": min(F, rt.abi.RT_MAX_BATCH),
-                             "row_block": BLOCK_ROWS, "output": surfaces[surf][3] + " shards gathered to rank 0",
+                             "row_block": BLOCK_ROWS,
+                             "output": (surfaces[surf][3] + (" shards, sent as RGB8 (the constant alpha byte dropped), "
+                                                             "gathered to rank 0" if surf == "rgba8" else
+                                                             " shards gathered to rank 0")),
                              "parallelism": "every frame row-tiled x%d in interleaved %d-row blocks + RCCL gather "
                                             "to rank 0, de-interleaved there, overlapped with the next render"
                                             % (world, BLOCK_ROWS)})

@@ -64,6 +64,47 @@ def assemble(flat, n_frames, height, width, block_rows, channels=4, perm=None):
     return np.concatenate(parts, axis=1)[:, perm]
 
 
+def contiguous_assembly_rows(n_frames, height, block_rows, n_shards):
+    """For a gather into ONE contiguous buffer of n_shards equal chunks (chunk
+    s = shard s's flat buffer, flat_shard_elems elements: (n_frames, rows_s,
+    width, channels) at its start): idx[f * height + r] = the buffer row (of
+    width * channels elements) holding frame f's row r. One index_select then
+    assembles every frame (`assemble_contiguous`), without first
+    concatenating the shards."""
+    padded = padded_shard_rows(height, block_rows, n_shards)
+    idx = np.empty((n_frames, height), np.int64)
+    for s in range(n_shards):
+        ids = shard_row_ids(height, block_rows, n_shards, s)
+        for f in range(n_frames):
+            idx[f, ids] = (s * n_frames * padded) + f * len(ids) + np.arange(len(ids))
+    return idx.reshape(-1)
+
+
+def assemble_contiguous(buf, n_frames, height, width, channels, idx):
+    """buf: the contiguous gather buffer (torch or numpy, flat); idx:
+    contiguous_assembly_rows. Returns (n_frames, height, width, channels)."""
+    rows = buf.reshape(-1, width * channels)
+    try:
+        import torch
+        if isinstance(buf, torch.Tensor):
+            i = idx if isinstance(idx, torch.Tensor) else torch.as_tensor(idx, device=buf.device)
+            return rows.index_select(0, i).reshape(n_frames, height, width, channels)
+    except ImportError:
+        pass
+    return rows[idx].reshape(n_frames, height, width, channels)
+
+
+def pack_rgb8(rgba8, out):
+    """The GL_RGBA8 texels (RT_OUTPUT_RGBA8, one 4-byte texel per pixel, any
+    integer dtype) without their alpha byte, which the reference stores as 0
+    (imageStore of vec4(rgb, 0.0), raytrace_compute.glsl:404): 3 bytes per
+    pixel into the uint8 tensor `out` (torch)."""
+    import torch
+    src = rgba8.view(torch.uint8).view(-1, 4)
+    out.view(-1, 3)[: src.shape[0]].copy_(src[:, :3])
+    return out
+
+
 def exchange_splits(height, width, block_rows, n_shards, rank, channels=4, frames_per_rank=1):
     """All-to-all split sizes (elements) for the frame exchange: this rank's
     batch buffer is (n_shards * F frames, rows_rank, width, channels), frames

@@ -39,7 +39,7 @@ def test_config2_two_ranks_row_tiled_gather():
     line = run_bench(2, "--steps", "3", "--warmup", "1", "--frames", "3")
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
     assert line["config"]["frames_per_step"] == 3 and "gather" in line["timing"]["collective"]
-    assert "GL_RGBA8" in line["config"]["output"]
+    assert "GL_RGBA8" in line["config"]["output"] and "RGB8" in line["config"]["output"]
     ranks = line["timing"]["per_rank"]
     assert [r["rank"] for r in ranks] == [0, 1] and all(r["kernel_ms"] > 0 and r["collective_ms"] > 0 for r in ranks)
     assert line["roofline"]["bytes_per_launch"] == 3 * 1920 * 544 * 4  # 4 B per pixel, rank 0: 68 of 135 8-row blocks

@@ -197,3 +197,44 @@ def test_rgba8_frames_gather_to_rank0(tmp_path, world):
     mp.start_processes(rgba8_gather_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
     full = np.stack([rt.pack_rgba8(oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, t)) for t in TIMES])
     assert np.array_equal(np.load(out), full)
+
+
+def rgb8_contiguous_worker(rank, world, port, result_path):
+    """bench.py config2's gather at N ranks: the GL_RGBA8 shards packed to
+    RGB8 (frame.pack_rgb8: the constant alpha byte dropped), gathered into
+    one contiguous buffer on rank 0 and de-interleaved by one index_select
+    (frame.contiguous_assembly_rows / assemble_contiguous)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import openglraytracer_amd as rt
+    from openglraytracer_amd import frame
+    from oracle import port as oracle_port, scenes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    objs = scenes.bench_objects(16)
+    ids = frame.shard_row_ids(H, BLOCK, world, rank)
+    px = frame.flat_shard_elems(FRAMES, H, W, BLOCK, world, channels=1)
+    texels = torch.zeros(px, dtype=torch.int32)
+    data = np.stack([rt.pack_rgba8(np.concatenate([oracle_port.render(objs, W, H, DEPTH, t, rows=(int(r), int(r) + 1))
+                                                   for r in ids])) for t in TIMES])
+    flat = np.ascontiguousarray(data).view(np.int32).reshape(-1)
+    texels[: flat.size] = torch.from_numpy(flat)
+    send = frame.pack_rgb8(texels, torch.empty(px * 3, dtype=torch.uint8))
+    big = torch.empty(world * px * 3, dtype=torch.uint8) if rank == 0 else None
+    dist.gather(send, [big[r * px * 3:(r + 1) * px * 3] for r in range(world)] if rank == 0 else None, dst=0)
+    if rank == 0:
+        idx = frame.contiguous_assembly_rows(FRAMES, H, BLOCK, world)
+        np.save(result_path, frame.assemble_contiguous(big, FRAMES, H, W, 3, idx).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rgb8_shards_gather_contiguously_to_rank0(tmp_path, world):
+    import openglraytracer_amd as rt
+    from oracle import port as oracle_port, scenes
+    out = str(tmp_path / "frames.npy")
+    mp.start_processes(rgb8_contiguous_worker, args=(world, free_port(), out), nprocs=world, start_method="spawn")
+    full = np.stack([rt.pack_rgba8(oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, t)) for t in TIMES])
+    assert np.all(full[..., 3] == 0)
+    assert np.array_equal(np.load(out), full[..., :3])
