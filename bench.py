@@ -361,16 +361,18 @@ def main():
         rows_mine = rt.shard_rows(H, BLOCK_ROWS, world, rank)
         elems = frame.flat_shard_elems(1, H, W, BLOCK_ROWS, world, ch)
         bufs = [torch.zeros(elems, dtype=dt, device="cuda") for _ in range(2)]
-        glists = ([[torch.empty(elems, dtype=dt, device=coll_dev) for _ in range(world)] for _ in bufs]
-                  if rank == 0 else None)
-        perm = torch.as_tensor(frame.assembly_permutation(H, BLOCK_ROWS, world), device=coll_dev)
+        # the gather lands in one contiguous buffer per slot; one index_select
+        # de-interleaves the frame
+        bigs = ([torch.empty(world * elems, dtype=dt, device=coll_dev) for _ in bufs] if rank == 0 else None)
+        idx = torch.as_tensor(frame.contiguous_assembly_rows(1, H, BLOCK_ROWS, world), device=coll_dev)
 
         def collective(slot, src):
-            dist.gather(src, glists[slot] if rank == 0 else None, dst=0)  # RCCL: every shard to rank 0
+            dist.gather(src, [bigs[slot][r * elems:(r + 1) * elems] for r in range(world)] if rank == 0 else None,
+                        dst=0)  # RCCL: every shard to rank 0
 
         def assemble(slot):
             if rank == 0:
-                return frame.assemble(glists[slot], 1, H, W, BLOCK_ROWS, channels=ch, perm=perm)
+                return frame.assemble_contiguous(bigs[slot], 1, H, W, ch, idx)
             return None
         return Plan(bufs, lambda buf: rt.render_shard(ctx, scene, buf.data_ptr(), W, H, DEPTH, BLOCK_ROWS, world,
                                                       rank, view=view, stream=sh),
