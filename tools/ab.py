@@ -3,10 +3,15 @@
     python tools/ab.py CONFIG[,CONFIG...] BUILD [BUILD ...]
 
 BUILD is a directory under _ab (tools/ablate.sh) or "main" for the
-in-tree library. Every build gets its own context and scene; each round times
-every build once (one event pair around REPS back-to-back launches on a
-non-default stream), rounds interleaved so clock drift hits all builds alike.
-Prints the median and min per-frame kernel time and a hash of the frame.
+in-tree library, optionally with context options (main:5=1 = RT_OPT_WAVEFRONT
+on). CONFIG is config1..config4, "config2x8" (8 animated frames per launch,
+rt_render_batch) or "config5" (Monte-Carlo, 16 jittered samples per launch).
+Every build gets its own context and scene; each round times every build once
+— REPS/2 untimed launches, then one event pair around REPS back-to-back
+launches on a non-default stream, about 60 ms of GPU work, so the clock is the
+sustained one the bench sees rather than a short burst's — rounds interleaved
+so clock drift hits all builds alike. Prints the median and min per-frame
+(per-sample) kernel time and a hash of the frame.
 """
 import ctypes as C
 import hashlib
