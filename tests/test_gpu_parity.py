@@ -936,3 +936,71 @@ def test_wavefront_config4_full_frame_slices_equal_walk(gpu_ctx):
     finally:
         gpu_ctx.set_wavefront(False)
         sc.close()
+
+
+# ---- randomised scenes ------------------------------------------------------
+def random_scene(seed):
+    """A seeded random scene: the room box or not, up to 3 extra rotated
+    boxes, 0-300 spheres (LDS direction masks, wide masks with candidate
+    lists and their overflow, per-wave shadow cones, the BVH), the reference
+    materials plus 2 random ones (mirrors, glass of random index, emissive,
+    shininess), 1-4 random lights (some dead: no diffuse / specular), the
+    reference orbit camera at a random time, a ragged frame and depth 0-5."""
+    rng = np.random.default_rng(1000 + seed)
+    mats = rt.reference_materials()
+    for _ in range(2):
+        m = rt.abi.Material()
+        m.ambient[:] = rng.uniform(0.0, 0.4, 4)
+        m.diffuse[:] = rng.uniform(0.0, 1.0, 4)
+        m.specular[:] = rng.uniform(0.0, 1.0, 4)
+        m.shininess = float(rng.uniform(1.0, 120.0))
+        m.emissive[:] = rng.uniform(0.0, 0.3, 4) if rng.random() < 0.3 else (0.0, 0.0, 0.0, 0.0)
+        m.reflectivity = float(rng.choice([0.0, 0.3, 1.0, rng.uniform(0.0, 1.0)]))
+        m.transparency = float(rng.choice([0.0, 0.5, rng.uniform(0.0, 1.0)]))
+        m.refraction_index = float(rng.uniform(1.0, 2.5))
+        mats.append(m)
+    lights = []
+    for _ in range(int(rng.integers(1, 5))):
+        lt = rt.abi.Light()
+        lt.position[:] = rng.uniform(-9.0, 9.0, 3)
+        lt.ambient[:] = rng.uniform(0.0, 0.2, 4)
+        if rng.random() < 0.25:  # dead: ambient only
+            lt.diffuse[:] = (0.0, 0.0, 0.0, 0.0)
+            lt.specular[:] = (0.0, 0.0, 0.0, 0.0)
+        else:
+            lt.diffuse[:] = rng.uniform(0.0, 1.0, 4)
+            lt.specular[:] = rng.uniform(0.0, 1.0, 4)
+        lights.append(lt)
+    objs = [scenes.room_box()] if rng.random() < 0.8 else []
+    for _ in range(int(rng.integers(0, 4))):
+        objs.append(scenes.box(tuple(-rng.uniform(0.2, 2.0, 3)), tuple(rng.uniform(0.2, 2.0, 3)),
+                               tuple(rng.uniform(-6.0, 6.0, 3)), tuple(rng.uniform(0.0, 360.0, 3)),
+                               int(rng.integers(len(mats)))))
+    n_sph = int(rng.choice([0, 5, 16, 40, 64, 100, 256, 300]))
+    for _ in range(n_sph):
+        objs.append(scenes.sphere(tuple(rng.uniform(-8.0, 8.0, 3)), float(rng.uniform(0.1, 1.5)),
+                                  int(rng.integers(len(mats)))))
+    t = float(rng.uniform(0.0, 20.0))
+    depth = int(rng.integers(0, 6)) if n_sph <= 64 else int(rng.integers(0, 4))
+    w, h = int(rng.integers(24, 100)), int(rng.integers(16, 70))
+    return objs, mats, lights, t, depth, w, h
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_random_scenes_match_oracle(gpu_ctx, seed):
+    """Seeded random scenes (random_scene), the product camera path at a
+    random time: bit-exact against the oracle, culling on and off."""
+    objs, mats, lights, t, depth, w, h = random_scene(seed)
+    view = rt.make_view(None, t)
+    sc = rt.Scene(gpu_ctx, objs, materials=mats, lights=lights)
+    try:
+        g = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+        gpu_ctx.set_culling(False)
+        off = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+    finally:
+        gpu_ctx.set_culling(True)
+        sc.close()
+    o = oracle_render(objs, w, h, depth, t, materials=mats, lights=lights)
+    desc = (seed, len(objs), len(lights), depth, w, h, round(t, 3))
+    assert np.array_equal(g, o, equal_nan=True), (desc, parity_stats(g, o))
+    assert np.array_equal(off, o, equal_nan=True), (desc, parity_stats(off, o))
