@@ -1004,3 +1004,44 @@ def test_random_scenes_match_oracle(gpu_ctx, seed):
     desc = (seed, len(objs), len(lights), depth, w, h, round(t, 3))
     assert np.array_equal(g, o, equal_nan=True), (desc, parity_stats(g, o))
     assert np.array_equal(off, o, equal_nan=True), (desc, parity_stats(off, o))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_scenes_batch_shards_rgba8_and_mc(gpu_ctx, seed):
+    """The same random scenes through the other launch shapes: three animated
+    views in one launch equal three single renders; interleaved row shards
+    reassemble the frame; the GL_RGBA8 surface equals rt_pack_rgba8 of the
+    float frame; two Monte-Carlo calls of 2 samples equal the oracle's
+    in-order sums."""
+    objs, mats, lights, t, depth, w, h = random_scene(seed)
+    times = [t, t + 0.5, t + 1.25]
+    views = [rt.make_view(None, x) for x in times]
+    sc = rt.Scene(gpu_ctx, objs, materials=mats, lights=lights)
+    try:
+        singles = [rt.render(gpu_ctx, sc, w, h, depth, view=v) for v in views]
+        batch = torch.zeros((3, h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch(gpu_ctx, sc, batch.data_ptr(), w, h, depth, views)
+        torch.cuda.synchronize()
+        for k in range(3):
+            assert np.array_equal(batch[k].cpu().numpy(), singles[k], equal_nan=True), (seed, k)
+        n = 3
+        got = np.zeros_like(singles[0])
+        for s in range(n):
+            buf = torch.zeros(rt.shard_rows(h, 4, n, s) * w * 4, dtype=torch.float32, device="cuda")
+            rt.render_shard(gpu_ctx, sc, buf.data_ptr(), w, h, depth, 4, n, s, view=views[0])
+            torch.cuda.synchronize()
+            got[frame.shard_row_ids(h, 4, n, s)] = buf.cpu().numpy().reshape(-1, w, 4)
+        assert np.array_equal(got, singles[0], equal_nan=True), seed
+        assert np.array_equal(rt.render_rgba8(gpu_ctx, sc, w, h, depth, view=views[0]), rt.pack_rgba8(singles[0]))
+        if depth <= 2:
+            acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+            rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 0, seed=seed, view=views[0])
+            rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 2, seed=seed, view=views[0])
+            torch.cuda.synchronize()
+            o = port.render_accumulate(objs, w, h, depth, 2, 0, seed=seed, time=times[0], materials=mats,
+                                       lights=lights)
+            o = port.render_accumulate(objs, w, h, depth, 2, 2, seed=seed, accum=o, time=times[0], materials=mats,
+                                       lights=lights)
+            assert np.array_equal(acc.cpu().numpy(), o, equal_nan=True), (seed, parity_stats(acc.cpu().numpy(), o))
+    finally:
+        sc.close()
