@@ -189,6 +189,9 @@ struct LaunchParams {
     // (host_frame_setup): n_frame_consts records per view, view k's at
     // k * n_frame_consts; 0: every work-group derives them.
     int32_t n_frame_consts;
+    // 1: every view's camera-ray perspective divisions take the short form,
+    // exact for every pixel (rt_scene.cpp camera_short_divisions)
+    int32_t cam_short;
     // Rows [slice_begin, slice_begin + slice_rows) of the launch's local rows
     // (the whole launch when slice_rows = 0); a wavefront frame runs slice by slice.
     int32_t slice_begin, slice_rows;

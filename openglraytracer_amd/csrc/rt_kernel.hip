@@ -1504,11 +1504,22 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
         ws[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 0.5f + M[12 + k] * 1.0f;
         we[k] = M[k] * vx + M[4 + k] * vy + M[8 + k] * 1.0f + M[12 + k] * 1.0f;
     }
-    // (the six perspective divisions as two shared refined reciprocals and
-    // one-correction quotients behind a per-wave range check measured slower
-    // again with the cheaper quotient: config 2 38.9 -> 40.3 us per frame)
-    const v3 s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
-    const v3 e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
+    // (the same short divisions behind a per-wave range check measured
+    // slower, config 2 38.9 -> 40.3 us per frame: the check is now made once
+    // per launch on the host and read as a uniform argument)
+    v3 s3, e3;
+    if (p.cam_short) {
+        // the host proved every numerator +0 or in [2^-60, 2^60] and every w
+        // in [2^-20, 2^20] for this frame (rt_scene.cpp camera_short_divisions):
+        // one refined reciprocal per w and one correction per quotient, the
+        // correctly rounded quotients (config 2 -3.2 %, config 5 -5.4 %, r03w)
+        const Rcp rs3 = rcp_refined(ws[3]), re3 = rcp_refined(we[3]);
+        s3 = mk(div_r(ws[0], rs3), div_r(ws[1], rs3), div_r(ws[2], rs3));
+        e3 = mk(div_r(we[0], re3), div_r(we[1], re3), div_r(we[2], re3));
+    } else {
+        s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
+        e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
+    }
     Ray ray;
     ray.start = mk(V.origin[0], V.origin[1], V.origin[2]);
     ray.dir = normalize(sub(e3, s3));

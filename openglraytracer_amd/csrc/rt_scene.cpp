@@ -512,6 +512,52 @@ bool view_projection(const rt_view &v, float proj[16]) {
     return ok;
 }
 
+// Whether the camera ray's six perspective divisions (raytrace_compute.glsl
+// :383-390, ws[k] / ws[3] and we[k] / we[3]) may take the short form
+// (rt_kernel.hip div_r: the refined reciprocal of the w component and one
+// correction, correctly rounded for b normal in [2^-60, 2^60] and a = +0 or
+// |a| in [2^-60, 2^60]) for EVERY pixel of a width x height frame, jittered
+// samples included. Each component is ((M[k] vx + M[4+k] vy) + M[8+k] z) +
+// M[12+k] in float32 with vx in [-1, (width - hw) / hw], vy likewise and z in
+// {0.5, 1}:
+//  * a numerator's last operation adds c = M[12+k] != 0 to a float y: a
+//    nonzero result is at least 2^-26 |c| (if |y| >= |c| / 2 both are
+//    multiples of ulp(c) / 2, else |y + c| > |c| / 2), and an exact
+//    cancellation gives +0, never -0; so |c| >= 2^-34 keeps every nonzero
+//    numerator at or above 2^-60;
+//  * the denominators are the linear function w(vx, vy, z) up to rounding:
+//    its extremes over the pixel box are at the corners (float64), and the
+//    float32 evaluation differs from it by at most 8 * 2^-24 times the sum
+//    of the terms' magnitudes; both sit in [2^-20, 2^20] or in the mirror
+//    range, every pixel's w does.
+bool camera_short_divisions(const float M[16], int width, int height) {
+    const int hw = width / 2, hh = height / 2;
+    if (hw <= 0 || hh <= 0) return false;
+    for (int i = 0; i < 16; ++i)
+        if (!std::isfinite(M[i]) || std::fabs(M[i]) > 0x1p40f) return false;
+    for (int k = 0; k < 4; ++k)
+        if (!(std::fabs(M[12 + k]) >= 0x1p-34f)) return false;
+    const double vx[2] = {-1.0, static_cast<double>(width - hw) / hw};
+    const double vy[2] = {-1.0, static_cast<double>(height - hh) / hh};
+    for (const double z : {0.5, 1.0}) {
+        const double mag = std::fabs(M[3]) * std::max(std::fabs(vx[0]), std::fabs(vx[1])) +
+                           std::fabs(M[7]) * std::max(std::fabs(vy[0]), std::fabs(vy[1])) + std::fabs(M[11]) * z +
+                           std::fabs(M[15]);
+        const double err = 8.0 * 0x1p-24 * mag + 0x1p-100;
+        double lo = INFINITY, hi = -INFINITY;
+        for (const double x : vx)
+            for (const double y : vy) {
+                const double w = double(M[3]) * x + double(M[7]) * y + double(M[11]) * z + double(M[15]);
+                lo = std::min(lo, w);
+                hi = std::max(hi, w);
+            }
+        const bool pos = lo - err >= 0x1p-20 && hi + err <= 0x1p20;
+        const bool neg = hi + err <= -0x1p-20 && lo - err >= -0x1p20;
+        if (!pos && !neg) return false;
+    }
+    return true;
+}
+
 // The kernel's frame_setup (rt_kernel.hip) for a one-view launch, on the
 // host: every work-group would otherwise derive the same constants (measured
 // 7 % of a 1080p depth-0 frame). Camera terms in float32 with the kernel's

@@ -347,3 +347,27 @@ def test_kernel_switch_compiles(flag):
            os.path.join(ROOT, "openglraytracer_amd", "csrc", "rt_kernel.hip")] + ([flag] if flag else [])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("t", [0.0, 1.0, 3.3, 7.25, 100.0])
+def test_camera_short_division_ranges_hold_on_real_frames(t):
+    """The short perspective divisions of the camera ray (rt_kernel.hip
+    camera_ray with p.cam_short; host proof rt_scene.cpp
+    camera_short_divisions) need every numerator +0 or in [2^-60, 2^60] and
+    every w in [2^-20, 2^20]: evaluated here in float32 with the kernel's
+    operation order for every pixel of the config 2-4 frames (rows
+    subsampled at 8K) of the reference camera, which the host accepts."""
+    view = rt.make_view(None, t)
+    M = np.array(view.unprojection[:], np.float32)
+    for w, h, step in ((1920, 1080, 1), (3840, 2160, 3), (7680, 4320, 17)):
+        hw, hh = w // 2, h // 2
+        vx = ((np.arange(w) - hw).astype(np.float32) / np.float32(hw))[None, :]
+        vy = ((np.arange(0, h, step) - hh).astype(np.float32) / np.float32(hh))[:, None]
+        for z in (np.float32(0.5), np.float32(1.0)):
+            comp = [((M[k] * vx + M[4 + k] * vy) + M[8 + k] * z) + M[12 + k] * np.float32(1.0) for k in range(4)]
+            for a in comp[:3]:
+                nz = a[a != 0]
+                assert not np.signbit(a[a == 0]).any()
+                assert (np.abs(nz) >= 2.0 ** -60).all() and (np.abs(nz) <= 2.0 ** 60).all()
+            wv = np.abs(comp[3])
+            assert (wv >= 2.0 ** -20).all() and (wv <= 2.0 ** 20).all()
