@@ -11,7 +11,10 @@ time k/60 s), rendered up to 8 frames per launch (rt_render_batch; SURVEY.md
 tail). The total work of a step is fixed: strong scaling.
   * N=1: every frame whole, float4 per pixel (16 B: the HBM-write roofline's
     bytes). The line also carries the one-frame-per-launch rate
-    (`single_frame`, the shape of the reference's draw(), main.cpp:228-238).
+    (`single_frame`, the shape of the reference's draw(), main.cpp:228-238),
+    and `rgba8_surface`: the same frames into the GL_RGBA8 surface that the
+    N>1 steps write, so the N=1 and N>1 points share a surface; every line's
+    roofline also carries `frac_float4_equivalent` (the pixels at 16 B).
   * N>1 (north_star: "image row-tiles shard across the GPUs with an RCCL
     gather over xGMI to assemble the frame"): every frame is row-tiled over
     the N ranks in interleaved 8-row blocks; each rank renders its blocks of
@@ -109,6 +112,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0,
                     help="approximate budget of the llvmpipe baseline samples")
+    ap.add_argument("--no-rgba8", action="store_true",
+                    help="config2 at N=1: skip the same-surface (GL_RGBA8) measurement")
     ap.add_argument("--no-single-frame", action="store_true",
                     help="config2: skip the one-frame-per-launch measurement (profiling runs: one launch shape)")
     return ap.parse_args()
@@ -485,7 +490,11 @@ def main():
         mismatch count is summed over the ranks that assemble."""
         bad, px = 0, 0
         if plan.last is not None:
-            ref = torch.zeros((n_frames, H, W, ch), dtype=dt, device="cuda")
+            # (empty: the render overwrites every pixel; torch's allocation
+            # and any fill would be queued on comm_s, which nothing orders
+            # before the synchronous render on the context's own stream)
+            ref = torch.empty((n_frames, H, W, ch), dtype=dt, device="cuda")
+            torch.cuda.synchronize()
             views = [rt.make_view(None, t) for t in times]
             for j in range(0, n_frames, rt.abi.RT_MAX_BATCH):
                 rt.render_batch(ctx, scene, ref[j].data_ptr(), W, H, DEPTH, views[j:j + rt.abi.RT_MAX_BATCH])
@@ -562,9 +571,27 @@ def main():
         extra["single_frame"] = {"frames_per_launch": 1, "us_per_frame": round(us, 3),
                                  "value": round(W * H / us, 3), "unit": "Mrays/s",
                                  "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
+    if batched and world == 1 and rank == 0 and not args.no_rgba8:
+        # the same F frames into the GL_RGBA8 surface the row-tiled N>1
+        # steps write (main.cpp:223): the same-surface point of the 1..8-GPU
+        # curve, with its 4-B and its float4-equivalent roofline
+        r8 = batch_plan("none", "rgba8")
+        e8, k8, _ = measure(r8, args.steps, args.warmup)
+        px8 = r8.px_per_launch
+        extra["rgba8_surface"] = {
+            "value": round(r8.rays_per_step * args.steps / e8 / 1e6, 3), "unit": "Mrays/s",
+            "ms_per_step": round(e8 / args.steps * 1e3, 5), "kernel_ms": round(k8, 5),
+            "frames_per_launch": px8 // (W * H), "output": "GL_RGBA8 surface (4 B per pixel), whole frames",
+            "roofline_frac": round(px8 * 4 / (k8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "roofline_frac_float4_equivalent": round(px8 * 16 / (k8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+        surface("rgba32f")
+        del r8
     ms_per_step = elapsed / args.steps * 1e3
     value = plan.rays_per_step * args.steps / elapsed / 1e6
     achieved = plan.px_per_launch * plan.bytes_per_pixel / (avg_kernel_ms * 1e-3) / 1e9
+    # the same pixels at 16 B each (the float4 frame of the N=1 line): one
+    # roofline scale for every point of a 1..8-GPU curve whatever its surface
+    achieved_f4 = plan.px_per_launch * 16 / (avg_kernel_ms * 1e-3) / 1e9
     fpl = plan.px_per_launch // (W * H) if batched and world == 1 else 1
     build = rt.lib().rt_version().decode()
     pmc = pmc_latest(wl, fpl, build) if world == 1 else {}
@@ -626,6 +653,7 @@ def main():
             "config": workload,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "frac_float4_equivalent": round(achieved_f4 / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_ms, 5),
                          "bytes_per_launch": plan.px_per_launch * plan.bytes_per_pixel,

@@ -171,7 +171,10 @@ int rt_scene_create(rt_context *ctx, const rt_object *objs, int n_objs, const rt
                     int n_mats, const rt_light *lights, int n_lights, rt_scene **out);
 /* Frees the scene's device memory in stream order behind every render that
  * reads it — on the context's stream and on any caller stream (an event per
- * stream is recorded at each render); no device-wide synchronisation. */
+ * stream is recorded at each render, for up to 8 distinct caller streams);
+ * no device-wide synchronisation, except when the scene was rendered on more
+ * than 8 distinct caller streams (or an event wait fails): then it waits for
+ * the whole device before freeing. rt_scene_update waits the same way. */
 void rt_scene_destroy(rt_scene *scene);
 /* Replace the scene's contents in place (an animated frame: the reference
  * recomputes its objects from `time` every frame, raytrace_compute.glsl:
@@ -298,14 +301,18 @@ int rt_multi_last_ms(rt_multi *m, float *kernel_ms, float *gather_ms, float *ass
  * 16 spheres + 1 box);
  * 0: every work-group derives them on the device. Output is identical. */
 #define RT_OPT_FRAME_CONSTS 4
-/* RT_OPT_WAVEFRONT (default 0): 1 renders frames of max_depth >= 2 (one
- * view, no Monte-Carlo accumulation) level by level — the camera rays, then
- * every bounce level's reflection and refraction rays from queues, then the
- * colour mixes bottom-up — instead of one depth-first walk per pixel; the
- * context then keeps a device work buffer for it (at most 8 GiB; larger
- * frames run in row slices). Output is identical; the depth-first walk (0)
- * measured about 2x faster on configs 3 and 4. */
-#define RT_OPT_WAVEFRONT 5
+/* RT_OPT_PRECISION (default RT_PRECISION_EXACT): RT_PRECISION_EXACT renders
+ * every pixel bit-identical to the reference's GL render (llvmpipe) of the
+ * same frame. RT_PRECISION_FAST is the tolerance tier: the same rays, with
+ * the recursion's colours accumulated forward (weights down the ray tree
+ * instead of nested mix() on the way back up, raytrace_compute.glsl:
+ * 1034-1054), within north_star's 1e-5 per channel of the reference on every
+ * GL fixture; it changes only max_depth >= 1 renders. */
+#define RT_OPT_PRECISION 6
+#define RT_PRECISION_EXACT 0
+#define RT_PRECISION_FAST 1
+/* (option 5, a level-by-level wavefront path for deep trees, was measured
+ * 2x slower than the depth-first walk and removed: DESIGN.md §3.) */
 int rt_context_set(rt_context *ctx, int option, int value);
 
 /* Kernel-only timing of the last render call (ms, from HIP events around the

@@ -193,47 +193,14 @@ struct LaunchParams {
     // exact for every pixel (rt_scene.cpp camera_short_divisions)
     int32_t cam_short;
     // Rows [slice_begin, slice_begin + slice_rows) of the launch's local rows
-    // (the whole launch when slice_rows = 0); a wavefront frame runs slice by slice.
+    // (the whole launch when slice_rows = 0).
     int32_t slice_begin, slice_rows;
-    // Wavefront path (depth >= 2, rt_kernel.hip launch_wavefront): the work
-    // buffer (wf_layout), its capacity in pixels of a slice, the frame's max
-    // depth and the level a trace / mix launch processes. nullptr: megakernel.
-    void *wf_base;
-    int32_t wf_cap, wf_depth, wf_level;
+    int32_t precision;  // RT_PRECISION_*: the exact kernels or the tolerance tier
     float4 frame_consts[kMaxFrameConsts];
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
 // MI355X); this block stays under 6 KiB.
 static_assert(sizeof(LaunchParams) <= 6144, "kernel argument block");
-// Wavefront work buffer (rt_kernel.hip, wavefront path) for a slice of P
-// pixels (whole 8x8 wave tiles: P = 64 * tiles) at max depth D. Queues are
-// sharded kWfShards ways — a wave appends to the shard of its chunk, so no
-// counter is hit by more than 1/64 of the appends (a single device-scope
-// counter serialises at ~88 atomics/us: r02). Layout: the counters (level,
-// kind, shard), each on its own 256-B line; the level-0 nodes (kWfShards x
-// cap(0)); then per level L = 1..D the rays and the nodes of reflection and
-// of refraction children (kWfShards x cap(L) each). 32 B per ray / node.
-// Shard capacities bound what can arrive: a chunk of 64 parents (a wave tile
-// at level 0) spawns at most 64 children of each kind into shard chunk % 64.
-constexpr int kWfShards = 64;
-constexpr int kWfLevels = RT_MAX_DEPTH + 1;
-constexpr size_t kWfCounterStride = 256;
-constexpr size_t kWfCounters = static_cast<size_t>(kWfLevels) * 2 * kWfShards * kWfCounterStride;
-constexpr size_t kWfRecord = 32;
-__host__ __device__ inline int64_t wf_shard_cap(int64_t pixels, int level) {
-    const int64_t n = level == 0 ? (pixels + kWfShards - 1) / kWfShards + 64
-                                 : ((pixels << (level - 1)) + kWfShards - 1) / kWfShards + 192;
-    return (n + 63) / 64 * 64;
-}
-// byte offset of part (0: rays R, 1: rays T, 2: nodes R, 3: nodes T; level 0: its nodes) of a level
-__host__ __device__ inline size_t wf_offset(int64_t pixels, int level, int part) {
-    size_t off = kWfCounters + kWfRecord * kWfShards * static_cast<size_t>(wf_shard_cap(pixels, 0));
-    for (int l = 1; l < level; ++l) off += 4 * kWfRecord * kWfShards * static_cast<size_t>(wf_shard_cap(pixels, l));
-    if (level > 0) off += static_cast<size_t>(part) * kWfRecord * kWfShards * static_cast<size_t>(wf_shard_cap(pixels, level));
-    return level == 0 ? kWfCounters : off;
-}
-inline size_t wf_buffer_bytes(int64_t pixels, int depth) { return wf_offset(pixels, depth + 1, 0); }
-constexpr size_t kWfBudget = size_t{8} << 30;  // work buffer of a context, at most (8 GiB of the GPU's 288)
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
 constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
 constexpr int kSchedInts = 2 * kQueues * kQueueStride; // heads + done counters of one launch
@@ -301,11 +268,7 @@ struct rt_context {
     int timing = 1;   // RT_OPT_TIMING
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int host_consts = 1;  // RT_OPT_FRAME_CONSTS
-    int wavefront = 0;    // RT_OPT_WAVEFRONT: depth >= 2 frames level by level (rt_kernel.hip)
-    void *wf_buf = nullptr;  // its work buffer (grown on demand)
-    size_t wf_bytes = 0;
-    hipEvent_t wf_done = nullptr;  // recorded after the last wavefront render (launches on other streams wait)
-    bool wf_used = false;
+    int precision = 0;    // RT_OPT_PRECISION
     int n_cu = 0;               // compute units of the device
     int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
     unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots

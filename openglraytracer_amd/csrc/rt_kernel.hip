@@ -1329,6 +1329,87 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
     }
 }
 
+// The tolerance tier's walk (RT_PRECISION_FAST, depth >= 1): the same rays in
+// the same order as trace_tree, with the colour accumulated forward. A node's
+// value mix(mix(phong, R, rho), T, tau) (each mix only for a spawned child) is
+// the weighted sum (1-rho')(1-tau') phong + rho'(1-tau') R + tau' T with
+// rho' = rho for a spawned reflection child, else 0 (tau' likewise), so the
+// pixel is the sum over its tree of weight x phong, a child's weight being its
+// parent's times rho'(1-tau') (reflection) or tau' (refraction). Nothing
+// waits for a subtree: only a node with BOTH children keeps a record — its
+// pending refraction ray and weight, 32 B — where trace_tree keeps a 40-B frame
+// for every node with children and reloads it on every return
+// (tools/model/walk_model.py, config 4: 10.1 instead of 29.9 frame rounds per
+// wave tile, 193 instead of 901 B of frame traffic per pixel). The rays are
+// bit-identical to trace_tree's; the colour differs by the rounding of a sum
+// instead of nested mixes (|d| <= 1e-5 per channel against every GL fixture,
+// tests/test_gpu_parity.py::test_fast_tier_*).
+struct Pending {
+    float4 rs_w;       // pending refraction ray start, its weight
+    float4 rd_level;   // its direction, its level (int bits)
+};
+template <int kDepth, class Emit>
+__device__ __forceinline__ void trace_tree_linear(const Scene &S, Ray ray, bool active, Emit &&emit) {
+    Pending stack[kDepth];
+    int sp = 0;
+    int level = 0;
+    float w = 1.0f;
+    v3 acc = mk(0.0f, 0.0f, 0.0f);
+    bool done = !active;
+    bool first = true;
+    while (__any(!done)) {
+        const bool valid = !done;
+        const bool primary = first;
+        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
+        first = false;
+        const bool hit = valid && h.obj >= 0;
+        const Collision c = primary ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
+        const v3 col = phong(S, ray, c, hit);
+        if (!valid) continue;
+        const MatRec &m = S.mat[c.material];
+        const bool sr = hit && level < kDepth && m.reflectivity > 0.0f;
+        const bool st = hit && level < kDepth && m.transparency > 0.0f;
+        const float rho = sr ? m.reflectivity : 0.0f, tau = st ? m.transparency : 0.0f;
+        const float keep = 1.0f - tau;
+        if (hit) acc = add(acc, muls(col, w * ((1.0f - rho) * keep)));  // a missed ray is black
+        if (sr || st) {
+            v3 rd = ray.dir;
+            if (__any(st)) {
+                const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
+                rd = refract(ray.dir, c.n, ratio);
+            }
+            const v3 rs = sub(c.p, muls(c.n, 0.001f));
+            if (sr && st) {  // the refraction child waits
+                stack[sp] = {make_float4(rs.x, rs.y, rs.z, w * tau),
+                             make_float4(rd.x, rd.y, rd.z, __int_as_float(level + 1))};
+                ++sp;
+            }
+            if (sr) {
+                ray.start = add(c.p, muls(c.n, 0.001f));
+                ray.dir = reflect(ray.dir, c.n);
+                w = w * (rho * keep);
+            } else {
+                ray.start = rs;
+                ray.dir = rd;
+                w = w * tau;
+            }
+            ++level;
+            continue;
+        }
+        if (sp > 0) {  // the deepest pending refraction child next
+            --sp;
+            const Pending q = stack[sp];
+            ray.start = mk(q.rs_w.x, q.rs_w.y, q.rs_w.z);
+            ray.dir = mk(q.rd_level.x, q.rd_level.y, q.rd_level.z);
+            w = q.rs_w.w;
+            level = __float_as_int(q.rd_level.w);
+            continue;
+        }
+        emit(acc);
+        done = true;
+    }
+}
+
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     if (p.n_shards <= 0) return p.row_begin + local;
     const int blk = local / p.block_rows;
@@ -1527,161 +1608,10 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
 }
 
 
-// ---- wavefront path for deep trees (max_depth >= 2) ----------------------
-// The stack machine (:848-1105) gives every node of a pixel's ray tree the
-// value mix(mix(phong, R, rho), T, tau) of its own Phong colour and its
-// children's values (each mix only for a spawned child, a missed ray black):
-// a node's value depends on its subtree alone, not on the order the tree is
-// walked. So instead of one depth-first walk per lane (trace_tree: frames in
-// scratch, every lane at its own tree position), a frame runs level by level:
-//  * level 0 (render_kernel<2, false, true>): the camera rays of the tiled
-//    kernel; a pixel whose hit spawns no child is stored at once, the others
-//    become level-0 nodes and push their children (wf_children);
-//  * levels 1..D (wf_trace_kernel): persistent waves take 64 rays at a time
-//    from the level's queues — reflection rays first, then refraction rays,
-//    each queue in the order its parents' waves pushed them, so a wave traces
-//    rays of one kind from neighbouring pixels — trace, shade, store their
-//    node and push the next level's children;
-//  * levels D-1..0 (wf_mix_kernel): every node with children mixes its
-//    children's final values into its own, bottom-up; level 0 stores the pixel.
-// Same device functions, same operations per node: bit-identical to
-// trace_tree (tests/test_gpu_parity.py renders both).
-// Nodes and rays are 32-B records in the context's work buffer, in
-// kWfShards shards per level and kind (rt_internal.h wf_offset): a wave
-// appends the nodes / children of its chunk to shard `chunk % 64`, and a
-// launch over a level maps its chunks of 64 onto the shards' counts with a
-// wave-wide prefix sum (one shard per lane) — no counter sees more than 1/64
-// of the appends, and no launch has a global head (static chunk
-// distribution: wave g takes chunks g, g + waves, ...).
-struct WfRay {
-    float4 o, d;  // start, direction (w unused)
-};
-struct WfNode {
-    float4 col;  // xyz: the node's value (phong, black on a miss; mixed in place), w: meta bits
-    int4 link;   // reflection child, refraction child (slots at level + 1; -1: none), level 0: output index
-};
-constexpr uint32_t kWfSr = 1u << 8, kWfSt = 1u << 9;  // meta: material | spawned children
-static_assert(kWfShards == 64, "one shard per lane of a wave");
-__device__ __forceinline__ int *wf_counter(const LaunchParams &p, int level, int kind, int shard) {
-    return reinterpret_cast<int *>(static_cast<char *>(p.wf_base) +
-                                   ((level * 2 + kind) * kWfShards + shard) * kWfCounterStride);
-}
-__device__ __forceinline__ WfRay *wf_rays(const LaunchParams &p, int level, int kind) {
-    return reinterpret_cast<WfRay *>(static_cast<char *>(p.wf_base) + wf_offset(p.wf_cap, level, kind));
-}
-__device__ __forceinline__ WfNode *wf_nodes(const LaunchParams &p, int level, int kind) {
-    return reinterpret_cast<WfNode *>(static_cast<char *>(p.wf_base) + wf_offset(p.wf_cap, level, level ? 2 + kind : 0));
-}
-// Wave-aggregated append (the calling lanes are those with `want`... all
-// lanes active): one atomic per wave; the lanes with `want` get consecutive
-// slots in lane order, the others -1.
-__device__ __forceinline__ int wave_append(int *counter, bool want) {
-    const uint64_t m = __ballot(want);
-    if (!m) return -1;
-    const int lane = threadIdx.x & 63, lead = __builtin_ctzll(m);
-    int base = 0;
-    if (lane == lead) base = atomicAdd(counter, __popcll(m));
-    base = __builtin_amdgcn_readlane(base, lead);
-    return want ? base + static_cast<int>(__popcll(m & ((uint64_t{1} << lane) - 1u))) : -1;
-}
-// Inclusive prefix sum over the 64 lanes (all active).
-__device__ __forceinline__ int wave_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int u = __shfl_up(v, d, 64);
-        if (lane >= d) v += u;
-    }
-    return v;
-}
-// A level's chunks of 64 records: reflection shards 0..63, then refraction
-// shards 0..63 (level 0: its nodes, kind 0 only); chunk c -> (kind, shard,
-// first record slot, records in the chunk).
-struct WfChunks {
-    int n_r, n_t;        // this lane's shard: records of each kind
-    int scan_r, scan_t;  // inclusive prefix sums of the shards' chunk counts
-    int total_r, total;  // chunks of kind 0, of both kinds
-    int64_t cap;         // shard capacity of the level
-};
-__device__ __forceinline__ WfChunks wf_chunks(const LaunchParams &p, int level) {
-    const int lane = threadIdx.x & 63;
-    WfChunks q;
-    q.n_r = *wf_counter(p, level, 0, lane);
-    q.n_t = level > 0 ? *wf_counter(p, level, 1, lane) : 0;
-    q.scan_r = wave_scan((q.n_r + 63) / 64);
-    q.scan_t = wave_scan((q.n_t + 63) / 64);
-    q.total_r = __builtin_amdgcn_readlane(q.scan_r, 63);
-    q.total = q.total_r + __builtin_amdgcn_readlane(q.scan_t, 63);
-    q.cap = wf_shard_cap(p.wf_cap, level);
-    return q;
-}
-// chunk c (wave-uniform, < q.total): kind, this lane's record slot, and
-// whether the lane has a record
-__device__ __forceinline__ void wf_chunk(const WfChunks &q, int c, int &kind, int &slot, bool &valid) {
-    const int lane = threadIdx.x & 63;
-    kind = c < q.total_r ? 0 : 1;
-    const int cc = kind ? c - q.total_r : c;
-    const int scan = kind ? q.scan_t : q.scan_r;
-    const int shard = static_cast<int>(__popcll(__ballot(scan <= cc)));  // shards wholly before chunk cc
-    const int before = shard ? __builtin_amdgcn_readlane(scan, shard - 1) : 0;
-    const int n = __builtin_amdgcn_readlane(kind ? q.n_t : q.n_r, shard);
-    const int i = (cc - before) * 64 + lane;
-    valid = i < n;
-    slot = static_cast<int>(shard * q.cap) + i;
-}
-// Push the children of this lane's node at `level` to level + 1 (the rays
-// trace_tree would start: :979-1030) and return their slots.
-__device__ __forceinline__ void wf_children(const LaunchParams &p, const Scene &S, int level, int shard,
-                                            const Ray &ray, const Collision &c, bool sr, bool st, int &cr, int &ct) {
-    const int cap = static_cast<int>(wf_shard_cap(p.wf_cap, level + 1));
-    cr = wave_append(wf_counter(p, level + 1, 0, shard), sr);
-    ct = wave_append(wf_counter(p, level + 1, 1, shard), st);
-    if (sr) cr += shard * cap;
-    if (st) ct += shard * cap;
-    if (sr) {
-        const v3 o = add(c.p, muls(c.n, 0.001f)), d = reflect(ray.dir, c.n);
-        wf_rays(p, level + 1, 0)[cr] = {make_float4(o.x, o.y, o.z, 0.0f), make_float4(d.x, d.y, d.z, 0.0f)};
-    }
-    if (st) {
-        const MatRec &m = S.mat[c.material];
-        const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
-        const v3 o = sub(c.p, muls(c.n, 0.001f)), d = refract(ray.dir, c.n, ratio);
-        wf_rays(p, level + 1, 1)[ct] = {make_float4(o.x, o.y, o.z, 0.0f), make_float4(d.x, d.y, d.z, 0.0f)};
-    }
-}
-// One ray per lane at `level` (all lanes active): closest hit, Phong, the
-// node's value and children. `store(value)`: a lane whose node spawns no
-// child at level 0 (its pixel is final); `node(value, meta, cr, ct)`: every
-// other lane with a ray (level 0: those that spawn).
-template <bool kPrimary, class Store, class Node>
-__device__ __forceinline__ void wf_trace(const LaunchParams &p, const Scene &S, int level, int shard, const Ray &ray,
-                                         bool valid, Store &&store, Node &&node) {
-    const v3 black = mk(0.0f, 0.0f, 0.0f);
-    const Hit h = closest<kPrimary>(S, ray, valid);
-    const bool hit = valid && h.obj >= 0;
-    Collision c;
-    c.material = 0;
-    v3 col = black;
-    bool sr = false, st = false;
-    if (__any(hit)) {
-        c = resolve<kPrimary>(S, ray, h, hit);
-        col = phong(S, ray, c, hit);
-        const MatRec &m = S.mat[c.material];
-        sr = hit && level < p.wf_depth && m.reflectivity > 0.0f;
-        st = hit && level < p.wf_depth && m.transparency > 0.0f;
-    }
-    const v3 value = hit ? col : black;  // a missed ray is black (:962-963)
-    int cr = -1, ct = -1;
-    if (__any(sr || st)) wf_children(p, S, level, shard, ray, c, sr, st, cr, ct);
-    const uint32_t meta = static_cast<uint32_t>(c.material) | (sr ? kWfSr : 0u) | (st ? kWfSt : 0u);
-    if (kPrimary && valid && !(sr || st)) store(value);
-    if (valid && (!kPrimary || sr || st)) node(value, meta, cr, ct);
-}
-
 // One 8x8 wave tile (wx, wy) of view z: lane l renders pixel (8 wx + l % 8,
 // 8 wy + l / 8). `pre`: the lane's camera ray, already computed (the tiled
 // path computes it while the scene is staged), or nullptr.
-template <int kDepth, bool kAccum, bool kWf>
+template <int kDepth, bool kAccum, bool kFast>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
@@ -1710,23 +1640,12 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 #elif defined(RT_ABLATE_TRACE)
         const v3 col = ray.dir;
 #else
-        if constexpr (kWf) {
-            // level 0 of a wavefront frame: pixels without children stored,
-            // the others become level-0 nodes (their output index kept)
-            const int shard = (wy * ((p.width + 7) / 8) + wx) % kWfShards;  // the wave tile's shard
-            wf_trace<true>(
-                p, S, 0, shard, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); },
-                [&](v3 col, uint32_t meta, int cr, int ct) {
-                    const int n = wave_append(wf_counter(p, 0, 0, shard), true) +
-                                  shard * static_cast<int>(wf_shard_cap(p.wf_cap, 0));
-                    wf_nodes(p, 0, 0)[n] = {make_float4(col.x, col.y, col.z, __uint_as_float(meta)),
-                                            make_int4(cr, ct, static_cast<int>(idx), 0)};
-                });
-            return;
-        }
         if constexpr (kDepth > 0) {
             // each lane's pixel stored as soon as its tree is finished
-            trace_tree<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
+            if constexpr (kFast)
+                trace_tree_linear<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
+            else
+                trace_tree<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
             return;
         }
         const v3 col = trace0(S, ray, active);
@@ -1742,7 +1661,10 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
             const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
             v3 col = mk(0.0f, 0.0f, 0.0f);
             if constexpr (kDepth == 0) col = trace0(S, camera_ray(p, V, x, y, jx, jy), active);
-            else trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active, [&](v3 c) { col = c; });
+            else if constexpr (kFast)
+                trace_tree_linear<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active, [&](v3 c) { col = c; });
+            else
+                trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active, [&](v3 c) { col = c; });
             acc = add(acc, col);
         }
         if (active) {
@@ -1776,10 +1698,10 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 // 52 -> 67 us, 8-frame launches, tiled either way, 41.5 -> 50.6 us per frame)
 constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 
-template <int kDepth, bool kAccum, bool kWf = false>
+template <int kDepth, bool kAccum, bool kFast>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    const bool queued = kQueuedDepth(kDepth) && !kWf && p.sched != nullptr;
+    const bool queued = kQueuedDepth(kDepth) && p.sched != nullptr;
     const int z = queued ? 0 : static_cast<int>(blockIdx.z);
     const FrameView &V = p.view[z];
     // wave index through readfirstlane: provably wave-uniform to the compiler,
@@ -1882,7 +1804,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
         int nxt = 0;
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
         const int wx = queued ? t % wtx : own_wx, wy = queued ? t / wtx : own_wy;
-        render_wave_tile<kDepth, kAccum, kWf>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
+        render_wave_tile<kDepth, kAccum, kFast>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
                                               own_ray, !(queued || kAccum));
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
@@ -1898,122 +1820,6 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     if (lane == 0 && atomicAdd(done, 1) == q_waves - 1) {
         atomicExch(head, 0);  // every wave of the queue has made its last fetch
         atomicExch(done, 0);
-    }
-}
-
-#ifndef RT_WPE_WF
-#define RT_WPE_WF 6
-#endif
-// Levels 1..D of a wavefront frame (see wf_trace): a grid of resident
-// work-groups, each staging the scene blob into LDS once; every wave then
-// traces 64-ray chunks of the level's queues (reflection rays, then
-// refraction rays; wf_chunks), chunks g, g + waves, ... of the level.
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(RT_WPE_WF))) void wf_trace_kernel(
-    LaunchParams p) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    const float4 *blob = static_cast<const float4 *>(p.scene);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    [[maybe_unused]] const int lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < p.blob_units; i += kThreads) lds[i] = blob[i];
-#ifdef RT_STATS
-    if (lane < kStats) rt_stats_lds[wave][lane] = 0u;
-#endif
-#ifdef RT_CYCLES
-    if (lane <= kCycPhases) rt_cyc_lds[wave][lane] = lane == kCycPhases ? __builtin_amdgcn_s_memtime() : 0u;
-    if (lane == 0) rt_cyc_cur[wave] = kCycPrologue;
-#endif
-    __syncthreads();
-    Scene S;
-    S.sph = lds + p.off_spheres;
-    S.smeta = reinterpret_cast<const int4 *>(lds + p.off_smeta);
-    S.sph_cam = nullptr;  // (camera-origin terms: primary rays only)
-    S.sph_px = nullptr;
-    S.box = reinterpret_cast<const BoxRec *>(lds + p.off_boxes);
-    S.box_cam = nullptr;
-    S.mat = reinterpret_cast<const MatRec *>(lds + p.off_mats);
-    S.light = reinterpret_cast<const LightRec *>(lds + p.off_lights);
-    S.lm = reinterpret_cast<const LightMatRec *>(lds + p.off_lightmat);
-    S.bvh = lds + p.off_bvh;
-    S.blink = reinterpret_cast<const uint32_t *>(lds + p.off_blink);
-    S.cone = p.off_cone >= 0 ? reinterpret_cast<const ShadowCone *>(lds + p.off_cone) : nullptr;
-    S.dmask = p.off_dmask >= 0 ? reinterpret_cast<const char *>(lds + p.off_dmask) : nullptr;
-    S.dmask_n = p.dmask_n;
-    S.dmask_bytes = p.dmask_bytes;
-    S.gmask = p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
-    S.gwords = p.gmask_words;
-    S.glist = S.gmask && p.off_glist >= 0 ? reinterpret_cast<const uint4 *>(blob + p.off_glist) : nullptr;
-    S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
-    S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
-    S.nbvh = p.n_bvh;
-    S.ns = p.n_spheres;
-    S.nb = p.n_boxes;
-    S.nl = p.n_lights;
-    S.nm = p.n_mats;
-    S.cull = p.view[0].cull;
-    S.tx0 = S.tx1 = S.ty0 = S.ty1 = 0;
-    const int level = p.wf_level;
-    const WfChunks q = wf_chunks(p, level);
-    const int n_waves = static_cast<int>(gridDim.x) * (kThreads / 64);
-    for (int c = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave; c < q.total; c += n_waves) {
-        int kind, slot;
-        bool valid;
-        wf_chunk(q, c, kind, slot, valid);
-        Ray ray{mk(0.0f, 0.0f, 0.0f), mk(0.0f, 0.0f, 1.0f)};
-        if (valid) {
-            const WfRay r = wf_rays(p, level, kind)[slot];
-            ray.start = mk(r.o.x, r.o.y, r.o.z);
-            ray.dir = mk(r.d.x, r.d.y, r.d.z);
-        }
-        WfNode *nodes = wf_nodes(p, level, kind);
-        wf_trace<false>(
-            p, S, level, c % kWfShards, ray, valid, [](v3) {},
-            [&](v3 col, uint32_t meta, int cr, int ct) {
-                nodes[slot] = {make_float4(col.x, col.y, col.z, __uint_as_float(meta)), make_int4(cr, ct, 0, 0)};
-            });
-    }
-#ifdef RT_STATS
-    if (lane < kStats) atomicAdd(&rt_stats[lane], static_cast<unsigned long long>(rt_stats_lds[wave][lane]));
-#endif
-#ifdef RT_CYCLES
-    RT_CYC(kCycStore);
-    if (lane < kCycPhases) atomicAdd(&rt_cycles[lane], rt_cyc_lds[wave][lane]);
-#endif
-    (void)wave;
-}
-
-// Levels D-1..0 of a wavefront frame, bottom-up: every node with children
-// takes mix(mix(value, R, rho), T, tau) over its spawned children (whose
-// values are final: their level ran before) (:1034-1054); level 0 stores
-// the pixel.
-__global__ __launch_bounds__(kThreads) void wf_mix_kernel(LaunchParams p) {
-    const int level = p.wf_level;
-    const MatRec *mat = reinterpret_cast<const MatRec *>(static_cast<const float4 *>(p.scene) + p.off_mats);
-    const WfChunks q = wf_chunks(p, level);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int n_waves = static_cast<int>(gridDim.x) * (kThreads / 64);
-    for (int c = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave; c < q.total; c += n_waves) {
-        int kind, slot;
-        bool valid;
-        wf_chunk(q, c, kind, slot, valid);
-        if (!valid) continue;
-        WfNode *nodes = wf_nodes(p, level, kind);
-        const WfNode nd = nodes[slot];
-        const uint32_t meta = __float_as_uint(nd.col.w);
-        if (!(meta & (kWfSr | kWfSt))) continue;  // a leaf: its value is final
-        const MatRec &m = mat[meta & 0xFFu];
-        v3 value = mk(nd.col.x, nd.col.y, nd.col.z);
-        if (meta & kWfSr) {
-            const float4 r = wf_nodes(p, level + 1, 0)[nd.link.x].col;
-            value = mix(value, mk(r.x, r.y, r.z), m.reflectivity);
-        }
-        if (meta & kWfSt) {
-            const float4 t = wf_nodes(p, level + 1, 1)[nd.link.y].col;
-            value = mix(value, mk(t.x, t.y, t.z), m.transparency);
-        }
-        if (level == 0)
-            store_pixel(p, 0, static_cast<uint32_t>(nd.link.z), value);
-        else
-            nodes[slot].col = make_float4(value.x, value.y, value.z, nd.col.w);
     }
 }
 
@@ -2039,10 +1845,10 @@ int groups_per_cu(const void *fn, size_t lds) {
     return n;
 }
 
-template <int kDepth, bool kAccum>
+template <int kDepth, bool kAccum, bool kFast>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
-    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
+    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum, kFast>);
     dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, p.n_views);
     const int wave_tiles = ((p.width + 7) / 8) * ((p.slice_rows + 7) / 8);
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
@@ -2054,46 +1860,19 @@ hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     } else {
         p.sched = nullptr;
     }
-    hipLaunchKernelGGL((render_kernel<kDepth, kAccum>), grid, dim3(kThreads), lds, stream, p);
+    hipLaunchKernelGGL((render_kernel<kDepth, kAccum, kFast>), grid, dim3(kThreads), lds, stream, p);
     return hipGetLastError();
-}
-
-// A wavefront frame (wf_trace): per slice of whole 8-row bands that fits the
-// work buffer (p.wf_cap pixels), the counters cleared, level 0, levels 1..D,
-// then the mixes D-1..0 — all queued on `stream`.
-hipError_t launch_wavefront(LaunchParams &p, int depth, hipStream_t stream) {
-    const int slice_rows = std::max(8, p.wf_cap / ((p.width + 7) / 8 * 8) / 8 * 8);
-    const size_t lds0 = lds_bytes(p), lds1 = static_cast<size_t>(p.blob_units) * sizeof(float4);
-    const void *trace_fn = reinterpret_cast<const void *>(&wf_trace_kernel);
-    const int resident = std::max(1, groups_per_cu(trace_fn, lds1) * std::max(p.n_cu, 1));
-    const int mix_groups = std::max(1, 4 * std::max(p.n_cu, 1));
-    p.sched = nullptr;
-    p.wf_level = 0;
-    for (int begin = 0; begin < p.n_rows; begin += slice_rows) {
-        p.slice_begin = begin;
-        p.slice_rows = std::min(slice_rows, p.n_rows - begin);
-        // the counters of levels 0..depth
-        hipError_t e = hipMemsetAsync(p.wf_base, 0, static_cast<size_t>(depth + 1) * 2 * kWfShards * kWfCounterStride,
-                                      stream);
-        if (e != hipSuccess) return e;
-        const dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, 1);
-        hipLaunchKernelGGL((render_kernel<2, false, true>), grid, dim3(kThreads), lds0, stream, p);
-        for (int level = 1; level <= depth; ++level) {
-            p.wf_level = level;
-            hipLaunchKernelGGL(wf_trace_kernel, dim3(resident), dim3(kThreads), lds1, stream, p);
-        }
-        for (int level = depth - 1; level >= 0; --level) {
-            p.wf_level = level;
-            hipLaunchKernelGGL(wf_mix_kernel, dim3(mix_groups), dim3(kThreads), 0, stream, p);
-        }
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    return hipSuccess;
 }
 
 template <int kDepth>
 hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
-    return p.spp > 0 ? launch_kernel<kDepth, true>(p, stream) : launch_kernel<kDepth, false>(p, stream);
+    // the tolerance tier (RT_PRECISION_FAST) differs from the exact kernels
+    // only where a ray tree is walked (trace_tree_linear, depth >= 1)
+    if constexpr (kDepth >= 1) {
+        if (p.precision == RT_PRECISION_FAST)
+            return p.spp > 0 ? launch_kernel<kDepth, true, true>(p, stream) : launch_kernel<kDepth, false, true>(p, stream);
+    }
+    return p.spp > 0 ? launch_kernel<kDepth, true, false>(p, stream) : launch_kernel<kDepth, false, false>(p, stream);
 }
 
 }  // namespace
@@ -2108,8 +1887,6 @@ hipError_t launch_render(LaunchParams &p, int max_depth, hipStream_t stream) {
         p.slice_begin = 0;
         p.slice_rows = p.n_rows;
     }
-    if (p.wf_base && max_depth >= 2 && p.n_views == 1 && p.spp == 0) return launch_wavefront(p, max_depth, stream);
-    p.wf_base = nullptr;
     switch (max_depth) {
         case 0: return launch_depth<0>(p, stream);
         case 1: return launch_depth<1>(p, stream);
@@ -2166,12 +1943,12 @@ int check_kernarg_block(hipStream_t stream) {
 // (gfx950 has 160 KiB per CU). Best effort: a failure only lowers the largest
 // scene that fits, which rt_scene_create checks.
 hipError_t allow_large_lds(size_t bytes) {
-#define RT_KFN(d) reinterpret_cast<const void *>(&render_kernel<d, false>), \
-                  reinterpret_cast<const void *>(&render_kernel<d, true>)
-    const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
-                         RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9),
-                         reinterpret_cast<const void *>(&render_kernel<2, false, true>),
-                         reinterpret_cast<const void *>(&wf_trace_kernel)};
+#define RT_KFN(d, f) reinterpret_cast<const void *>(&render_kernel<d, false, f>), \
+                     reinterpret_cast<const void *>(&render_kernel<d, true, f>)
+#define RT_KFN2(d) RT_KFN(d, false), RT_KFN(d, true)
+    const void *fns[] = {RT_KFN(0, false), RT_KFN2(1), RT_KFN2(2), RT_KFN2(3), RT_KFN2(4),
+                         RT_KFN2(5), RT_KFN2(6), RT_KFN2(7), RT_KFN2(8), RT_KFN2(9)};
+#undef RT_KFN2
 #undef RT_KFN
     for (const void *f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
@@ -2214,7 +1991,7 @@ extern "C" int rt_debug_phase_read(void *dst, size_t bytes) {
 }
 extern "C" int rt_debug_occupancy(size_t lds) {
     int n = -1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&rtamd::render_kernel<0, false>),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&rtamd::render_kernel<0, false, false>),
                                                      rtamd::kThreads, lds) != hipSuccess)
         return -1;
     return n;

@@ -1016,13 +1016,18 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         for (size_t t = 0; t < n_texels; ++t) {
             uint8_t *rec = glist.data() + t * 16;
             int n = 0;
-            for (int w = 0; w < ds.gmask_words; ++w)
-                for (uint64_t bits = gmask[t * ds.gmask_words + w]; bits; bits &= bits - 1) {
-                    const int s = 64 * w + __builtin_ctzll(bits);
-                    if (s >= static_cast<int>(sph.size())) break;
-                    if (n < kGListMax) rec[1 + n] = static_cast<uint8_t>(s);
+            // the same truncation as the kernel's word walk (occluded: the
+            // last word masked to the `rest` = ns - 64 w live slots)
+            const int ns = static_cast<int>(sph.size());
+            for (int w = 0; w < ds.gmask_words; ++w) {
+                uint64_t bits = gmask[t * ds.gmask_words + w];
+                const int rest = ns - 64 * w;
+                if (rest < 64) bits &= (uint64_t{1} << rest) - 1u;
+                for (; bits; bits &= bits - 1) {
+                    if (n < kGListMax) rec[1 + n] = static_cast<uint8_t>(64 * w + __builtin_ctzll(bits));
                     ++n;
                 }
+            }
             rec[0] = n <= kGListMax ? static_cast<uint8_t>(n) : static_cast<uint8_t>(kGListOverflow);
         }
         ds.off_glist = off;

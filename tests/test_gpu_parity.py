@@ -812,6 +812,34 @@ def test_scene_update_waits_for_renders_on_other_streams(gpu_ctx):
         sc.close()
 
 
+def test_scene_used_on_more_than_eight_streams(gpu_ctx):
+    """Past rt_scene::kMaxUseStreams (8) distinct caller streams the scene
+    stops recording per-stream events and rt_scene_update / rt_scene_destroy
+    fall back to a device-wide synchronisation (rt.h): renders queued on 10
+    torch streams, then an update and a destroy right behind them, leave
+    every frame intact."""
+    objs_a, objs_b = scenes.bench_objects(64), scenes.bench_objects(64, 7)
+    w, h, depth = 640, 360, 2
+    view = rt.make_view(None, 0.0)
+    want_a = gpu_render(gpu_ctx, objs_a, w, h, depth, view)
+    want_b = gpu_render(gpu_ctx, objs_b, w, h, depth, view)
+    streams = [torch.cuda.Stream() for _ in range(10)]
+    sc = rt.Scene(gpu_ctx, objs_a)
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in streams]
+    for o, s in zip(outs, streams):
+        rt.render_device(gpu_ctx, sc, o.data_ptr(), w, h, depth, view=view, stream=s.cuda_stream)
+    sc.update(objs_b)  # must wait for all ten renders of objs_a
+    outs_b = [torch.empty_like(outs[0]) for _ in streams]
+    for o, s in zip(outs_b, streams):
+        rt.render_device(gpu_ctx, sc, o.data_ptr(), w, h, depth, view=view, stream=s.cuda_stream)
+    sc.close()  # the renders of objs_b may still be running
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy(), want_a)
+    for o in outs_b:
+        assert np.array_equal(o.cpu().numpy(), want_b)
+
+
 STRAT = __import__("conftest").strat_manifest()
 
 
@@ -846,96 +874,6 @@ def test_stratified_crops_product_path_matches_gl(gpu_ctx, name):
     for (r0, r1), g in bands.items():
         o = oracle_render(objs, w, h, depth, m["time"], rows=(r0, r1))
         assert np.array_equal(g, o), (name, r0, parity_stats(g, o))
-
-
-# ---- wavefront path (RT_OPT_WAVEFRONT, rt_kernel.hip wf_*) -----------------
-def render_both_walks(ctx, objs, w, h, depth, view, rows=None, shard=None):
-    """The same frame through the level-by-level wavefront path and through
-    the per-pixel depth-first walk (the default)."""
-    sc = rt.Scene(ctx, objs)
-    out = []
-    try:
-        for on in (True, False):
-            ctx.set_wavefront(on)
-            if shard is None:
-                out.append(rt.render(ctx, sc, w, h, depth, view=view, rows=rows))
-            else:
-                block, n, s = shard
-                buf = torch.zeros(rt.shard_rows(h, block, n, s) * w * 4, dtype=torch.float32, device="cuda")
-                rt.render_shard(ctx, sc, buf.data_ptr(), w, h, depth, block, n, s, view=view)
-                torch.cuda.synchronize()
-                out.append(buf.cpu().numpy().reshape(-1, w, 4))
-    finally:
-        ctx.set_wavefront(False)
-        sc.close()
-    return out
-
-
-@pytest.mark.parametrize("cfg,w,h,depth", [("config3", 640, 360, 2), ("config4", 512, 288, 4), ("config4", 320, 180, 6),
-                                           ("config1", 160, 90, 9), ("config3", 37, 19, 3)])
-def test_wavefront_equals_depth_first_walk_and_oracle(gpu_ctx, cfg, w, h, depth):
-    """Level-by-level evaluation of every pixel's ray tree (each node's value
-    mixed from its children's, bottom-up) is bit-identical to the depth-first
-    stack-machine walk (raytrace_compute.glsl:848-1105) and to the oracle, at
-    depths 2-9 and ragged frame sizes."""
-    objs = scenes.CONFIGS[cfg][0]()
-    view = rt.make_view(None, 0.0)
-    wf, walk = render_both_walks(gpu_ctx, objs, w, h, depth, view)
-    assert np.array_equal(wf, walk), parity_stats(wf, walk)
-    o = oracle_render(objs, w, h, depth)
-    assert np.array_equal(wf, o), parity_stats(wf, o)
-
-
-def test_wavefront_shipped_scene_and_edge_objects(gpu_ctx):
-    """The shipped scene (rotated, animated boxes) at depth 4 and a scene of
-    degenerate spheres at depth 3, both ways and against the oracle."""
-    for objs, t, depth in ((rt.reference_objects(3.7), 3.7, 4), (scenes.bench_objects(40, seed=5), 0.0, 3)):
-        if depth == 3:
-            objs[3].radius = float("nan")
-            objs[7].position[0] = float("inf")
-            objs[11].radius = -1.5
-        view = rt.make_view(None, t)
-        wf, walk = render_both_walks(gpu_ctx, objs, 160, 90, depth, view)
-        assert np.array_equal(wf, walk, equal_nan=True), parity_stats(wf, walk)
-        o = oracle_render(objs, 160, 90, depth, t)
-        assert np.array_equal(wf, o, equal_nan=True), parity_stats(wf, o)
-
-
-def test_wavefront_row_bands_and_shards(gpu_ctx):
-    """Row bands and interleaved multi-GPU shards go through the wavefront
-    path too: each equals the same rows of the depth-first walk."""
-    objs = scenes.bench_objects(64)
-    w, h, depth = 800, 450, 3
-    view = rt.make_view(None, 0.0)
-    wf, walk = render_both_walks(gpu_ctx, objs, w, h, depth, view, rows=(101, 333))
-    assert np.array_equal(wf, walk)
-    for s in range(3):
-        a, b = render_both_walks(gpu_ctx, objs, w, h, depth, view, shard=(8, 3, s))
-        assert np.array_equal(a, b)
-        assert np.array_equal(a, rt.render(gpu_ctx, rt.Scene(gpu_ctx, objs), w, h, depth, view=view)[
-            frame.shard_row_ids(h, 8, 3, s)])
-
-
-def test_wavefront_config4_full_frame_slices_equal_walk(gpu_ctx):
-    """Config 4 at full size: the wavefront frame (rendered in row slices
-    that fit the context's work buffer) equals the depth-first walk bit for
-    bit over the whole 7680x4320 frame."""
-    build, w, h, depth = scenes.CONFIGS["config4"]
-    objs = build()
-    view = rt.make_view(None, 0.0)
-    sc = rt.Scene(gpu_ctx, objs)
-    try:
-        outs = []
-        for on in (True, False):
-            gpu_ctx.set_wavefront(on)
-            out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
-            rt.render_device(gpu_ctx, sc, out.data_ptr(), w, h, depth, view=view)
-            torch.cuda.synchronize()
-            outs.append(out)
-        assert torch.equal(outs[0], outs[1])
-    finally:
-        gpu_ctx.set_wavefront(False)
-        sc.close()
 
 
 # ---- randomised scenes ------------------------------------------------------

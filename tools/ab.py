@@ -3,8 +3,8 @@
     python tools/ab.py CONFIG[,CONFIG...] BUILD [BUILD ...]
 
 BUILD is a directory under _ab (tools/ablate.sh) or "main" for the
-in-tree library, optionally with context options (main:5=1 = RT_OPT_WAVEFRONT
-on). CONFIG is config1..config4, "config2x8" (8 animated frames per launch,
+in-tree library, optionally with context options (main:1=0 = RT_OPT_CULLING
+off). CONFIG is config1..config4, "config2x8" (8 animated frames per launch,
 rt_render_batch) or "config5" (Monte-Carlo, 16 jittered samples per launch).
 Every build gets its own context and scene; each round times every build once
 — REPS/2 untimed launches, then one event pair around REPS back-to-back
@@ -33,7 +33,7 @@ ROUNDS = 7
 
 def load(spec):
     # BUILD[:OPTION=VALUE...]: context options (rt_context_set) after the
-    # build name, e.g. main:5=0 (RT_OPT_WAVEFRONT off)
+    # build name, e.g. main:1=0 (RT_OPT_CULLING off)
     name, *opts = spec.split(":")
     path = rt.LIB_PATH if name == "main" else os.path.join(ROOT, "_ab", name, "libopenglraytracer_amd.so")
     L = C.CDLL(path)

@@ -34,6 +34,7 @@ fi
 if want prof5; then
   step prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
 fi
+if want shards; then step shard_timing 600 python tools/shard_timing.py; fi
 if want cycles; then step cycles 300 python tools/cycles.py cycles config2 config3 config4; fi
 if want stats; then step stats 300 python tools/stats.py stats config2 config3 config4; fi
 if want ab; then  # tools/ab.py over the builds under _ab/ (tools/ablate.sh)

@@ -5,12 +5,9 @@ gfx950 corrections of /opt/skills/guides/MI355X_MICROARCH.md (§HBM):
 WRITE_SIZE (KiB) is exact for 16-B-per-lane streaming stores; FETCH_SIZE
 reports half the bytes of a wide coalesced read, so it is doubled.
 
-A frame of a deep config on the wavefront path is several kernels
-(render_kernel<2, false, true> per row slice, wf_trace_kernel per level,
-wf_mix_kernel per level): with --frames N every figure is the sum over all
-the frame's render kernels' dispatches divided by the N frames the profiled
-bench run rendered (its --steps + --warmup), i.e. per frame; without it, per
-dispatch of the one render kernel.
+With --frames N every figure is the sum over all the render kernel's
+dispatches divided by the N frames the profiled bench run rendered (its
+--steps + --warmup), i.e. per frame; without it, per dispatch.
 
 usage: python tools/pmc_summary.py SRC DST [FRAMES_PER_LAUNCH] [WORKLOAD] [--frames N]
 (FRAMES_PER_LAUNCH: views per render launch of the profiled bench run, default 8;
@@ -34,7 +31,7 @@ if "--frames" in argv:
 src, dst = argv[0], argv[1]
 frames_per_launch = int(argv[2]) if len(argv) > 2 else 8
 workload = argv[3] if len(argv) > 3 else "config2"
-KERNELS = ("render_kernel", "wf_trace_kernel", "wf_mix_kernel")
+KERNELS = ("render_kernel",)
 
 
 def ours(name):
