@@ -89,6 +89,9 @@ __device__ __forceinline__ Rcp rcp_refined(float b) {
     return {b, r};
 }
 __device__ __forceinline__ float div_r(float a, Rcp d) {
+#ifdef RT_FAST_MATH
+    return a * __builtin_amdgcn_rcpf(d.b);
+#endif
     const float q = a * d.r;
     return __builtin_fmaf(__builtin_fmaf(-d.b, q, a), d.r, q);
 }
@@ -98,9 +101,20 @@ __device__ __forceinline__ float sqrt_short(float x) {
     const float r = __builtin_fmaf(-dn, s, x) <= 0.0f ? dn : s;
     return __builtin_fmaf(-up, s, x) > 0.0f ? up : r;
 }
+// a / b: the IEEE division (RT_FAST_MATH ablation builds: a * v_rcp(b))
+__device__ __forceinline__ float fdiv(float a, float b) {
+#ifdef RT_FAST_MATH
+    return a * __builtin_amdgcn_rcpf(b);
+#else
+    return a / b;
+#endif
+}
 // 1 / sqrt(d), both correctly rounded (GLSL inversesqrt as llvmpipe evaluates
 // it): the refined reciprocal of the short square root
 __device__ __forceinline__ float inv_sqrt(float d) {
+#ifdef RT_FAST_MATH
+    return __builtin_amdgcn_rsqf(d);
+#endif
     if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return rcp_refined(sqrt_short(d)).r;
     return 1.0f / sqrtf(d);
 }
@@ -127,6 +141,9 @@ __device__ __forceinline__ float inv_sqrt_near_one(float d) {
 // is within 2048 ulps of 1, else the general path; bit-identical either way
 __device__ __forceinline__ v3 normalize_unit(v3 a) {
     const float d = dot(a, a);
+#ifdef RT_FAST_MATH
+    return muls(a, __builtin_amdgcn_rsqf(d));
+#endif
     if (__all(near_one(d))) return muls(a, inv_sqrt_near_one(d));
     return muls(a, inv_sqrt(d));
 }
@@ -193,6 +210,9 @@ __device__ __forceinline__ float glsl_pow(float x, float y) { return glsl_exp2(g
 // vectors is at most about 3 or NaN, so glsl_log2's NaN and +inf cases are
 // never reached; its zero case becomes a select
 __device__ __forceinline__ float glsl_pow_cos(float x, float y) {
+#ifdef RT_FAST_MATH
+    return x == 0.0f ? 0.0f : __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+#endif
     const uint32_t i = __float_as_uint(x);
     const float e = static_cast<float>(static_cast<int>((i >> 23) & 0xffu) - 127);
     const float mant = __uint_as_float((i & 0x007fffffu) | 0x3f800000u);
@@ -380,8 +400,8 @@ __device__ __forceinline__ Slab slab(const BoxRec &b, v3 rs, v3 rd) {
     Slab s;
     s.rs = rs;
     s.rd = rd;
-    const v3 tmn = mk((b.mins[0] - rs.x) / rd.x, (b.mins[1] - rs.y) / rd.y, (b.mins[2] - rs.z) / rd.z);
-    const v3 tmx = mk((b.maxs[0] - rs.x) / rd.x, (b.maxs[1] - rs.y) / rd.y, (b.maxs[2] - rs.z) / rd.z);
+    const v3 tmn = mk(fdiv(b.mins[0] - rs.x, rd.x), fdiv(b.mins[1] - rs.y, rd.y), fdiv(b.mins[2] - rs.z, rd.z));
+    const v3 tmx = mk(fdiv(b.maxs[0] - rs.x, rd.x), fdiv(b.maxs[1] - rs.y, rd.y), fdiv(b.maxs[2] - rs.z, rd.z));
     s.t1 = mk(gmin(tmn.x, tmx.x), gmin(tmn.y, tmx.y), gmin(tmn.z, tmx.z));
     s.t2 = mk(gmax(tmn.x, tmx.x), gmax(tmn.y, tmx.y), gmax(tmn.z, tmx.z));
     s.t_near = gmax(gmax(s.t1.x, s.t1.y), s.t1.z);
@@ -408,7 +428,7 @@ __device__ __forceinline__ float exit_num(float mn, float mx, float s, float d) 
 __device__ __forceinline__ v3 exits(const BoxRec &b, v3 rs, v3 rd) {
     const float ex = exit_num(b.mins[0], b.maxs[0], rs.x, rd.x), ey = exit_num(b.mins[1], b.maxs[1], rs.y, rd.y),
                 ez = exit_num(b.mins[2], b.maxs[2], rs.z, rd.z);
-    return mk(ex / rd.x, ey / rd.y, ez / rd.z);
+    return mk(fdiv(ex, rd.x), fdiv(ey, rd.y), fdiv(ez, rd.z));
 }
 // Box t for the closest-hit loop (-1 on a miss), with the slab distances the
 // collision record's face test needs (bnd: t1 when entering, t2 when leaving)
@@ -433,7 +453,7 @@ __device__ __forceinline__ bool quotient_below_one(float num, float d) {
         if (an > ad * 1.0000153f) return false;
         if (an < ad * 0.9999847f) return true;
     }
-    return num / d < 1.0f;
+    return fdiv(num, d) < 1.0f;
 }
 // Does the box hold an occluder with 0 < t < 1 (:813-816)? light_bit: the
 // light is inside the box with a margin (host, float64), so a segment that
@@ -484,6 +504,9 @@ __device__ __forceinline__ float root_floor(float qa2) {
 // active lane's operand is in its range (qd >= 2^-96; +inf included), else
 // the IEEE sequence (config 4 18.20 -> 17.94 ms, config 3 1.030 -> 1.001 ms)
 __device__ __forceinline__ float sphere_sqrt(float qd) {
+#ifdef RT_FAST_MATH
+    return __builtin_amdgcn_sqrtf(qd);
+#endif
     if (__all(qd >= 0x1p-96f)) return sqrt_short(qd);
     return sqrtf(qd);
 }
@@ -498,10 +521,10 @@ __device__ __forceinline__ float sphere_t(float qb, float qc, float qa2, float q
         // slower: config 4 16.57 -> 16.79 ms)
         if (n1 < 0.0f) return -1.0f;  // t_far < 0
         inside = n2 < 0.0f;           // t_near < 0
-        return (inside ? n1 : n2) / qa2;
+        return fdiv(inside ? n1 : n2, qa2);
     }
-    const float t1 = n1 / qa2;
-    const float t2 = n2 / qa2;
+    const float t1 = fdiv(n1, qa2);
+    const float t2 = fdiv(n2, qa2);
     const float tn = gmin(t1, t2), tf = gmax(t1, t2);
     if (tf < 0.0f) return -1.0f;
     inside = tn < 0.0f;
@@ -1598,8 +1621,8 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
         s3 = mk(div_r(ws[0], rs3), div_r(ws[1], rs3), div_r(ws[2], rs3));
         e3 = mk(div_r(we[0], re3), div_r(we[1], re3), div_r(we[2], re3));
     } else {
-        s3 = mk(ws[0] / ws[3], ws[1] / ws[3], ws[2] / ws[3]);
-        e3 = mk(we[0] / we[3], we[1] / we[3], we[2] / we[3]);
+        s3 = mk(fdiv(ws[0], ws[3]), fdiv(ws[1], ws[3]), fdiv(ws[2], ws[3]));
+        e3 = mk(fdiv(we[0], we[3]), fdiv(we[1], we[3]), fdiv(we[2], we[3]));
     }
     Ray ray;
     ray.start = mk(V.origin[0], V.origin[1], V.origin[2]);

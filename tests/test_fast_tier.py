@@ -48,8 +48,10 @@ def tier_stats(got, ref):
     assert np.array_equal(np.isnan(g), np.isnan(r)), "NaN pixels differ"
     d = np.where(nan, 0.0, np.abs(g - r))
     scale = np.maximum(1.0, np.where(nan, 0.0, np.abs(r)))
-    rgba_g = rt.pack_rgba8(np.nan_to_num(got.astype(np.float32), nan=0.0))
-    rgba_r = rt.pack_rgba8(np.nan_to_num(ref.astype(np.float32), nan=0.0))
+    def rgba(x):  # (the GL fixtures hold RGB only; the alpha the shader stores is 0)
+        x = np.nan_to_num(x[..., :3].astype(np.float32), nan=0.0)
+        return rt.pack_rgba8(np.concatenate([x, np.zeros(x.shape[:-1] + (1,), np.float32)], -1))
+    rgba_g, rgba_r = rgba(got), rgba(ref)
     return {"max": float(d.max(initial=0.0)), "mean": float(d.mean()) if d.size else 0.0,
             "p99": float(np.percentile(d, 99)) if d.size else 0.0,
             "px_gt_1e5": int((d.max(-1) > TOL).sum()), "worst_ratio": float((d / (TOL * scale)).max(initial=0.0)),

@@ -40,4 +40,6 @@ if want stats; then step stats 300 python tools/stats.py stats config2 config3 c
 if want ab; then  # tools/ab.py over the builds under _ab/ (tools/ablate.sh)
   step ab 900 python tools/ab.py ${AB_ARGS:-}
 fi
+if want ab2; then step ab2 900 python tools/ab.py ${AB_ARGS2:-}; fi
+if want acc; then step accuracy 600 python tools/ab_accuracy.py ${ACC_ARGS:-main}; fi
 echo done

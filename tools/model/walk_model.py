@@ -138,7 +138,7 @@ def build_trees(S, w, h, depth, tiles, rng):
     ys = ((pick // wtx)[:, None] * 8 + lane // 8).reshape(-1).astype(np.float64)
     o, d = camera_rays(w, h, xs, ys)
     n_pix = len(xs)
-    pix, lev, hitl, cr, ct = [], [], [], [], []
+    pix, lev, hitl, cr, ct, ro, rd = [], [], [], [], [], [], []
     cur = dict(o=o, d=d, pix=np.arange(n_pix), parent=-np.ones(n_pix, int), kind=np.zeros(n_pix, int))
     base = 0
     for level in range(depth + 1):
@@ -148,6 +148,8 @@ def build_trees(S, w, h, depth, tiles, rng):
         hit, p, nrm, inside, mat = trace(S, cur["o"], cur["d"])
         ids = base + np.arange(m)
         pix.append(cur["pix"])
+        ro.append(cur["o"])
+        rd.append(cur["d"])
         lev.append(np.full(m, level))
         hitl.append(hit)
         cr.append(-np.ones(m, int))
@@ -176,21 +178,25 @@ def build_trees(S, w, h, depth, tiles, rng):
     cr, ct = np.concatenate(cr), np.concatenate(ct)
     for kind, par, child in links:
         (cr if kind == 0 else ct)[par] = child
+    build_trees.rays = (np.concatenate(ro), np.concatenate(rd))
     return n_pix, pix, lev, hitl, cr, ct
 
 
 links = []
 
 
-def lane_events(root, cr, ct):
+def lane_events(root, cr, ct, order=None):
     """The walk of one pixel, one entry per loop iteration (one traced ray):
-    (exact stores, exact loads, linear stores, linear loads)."""
+    (exact stores, exact loads, linear stores, linear loads); `order`
+    (a list) receives the node traced at each iteration."""
     ev = []
     # exact walk: explicit stack of (node, state) as trace_tree does
     stack = []  # frames: node ids with flag: waiting for R (2) or T (4)
     node = root
     lin_pending = 0
     while True:
+        if order is not None:
+            order.append(node)
         kids_r, kids_t = cr[node], ct[node]
         es = el = ls = ll = 0
         if kids_r >= 0 or kids_t >= 0:
