@@ -55,6 +55,25 @@ def gpu_ctx():
     ctx.close()
 
 
+def dev_zeros(*shape, dtype=None, device="cuda"):
+    """A zero-filled device tensor whose fill has completed: torch queues the
+    fill on its current stream, which nothing orders before a render on the
+    library's own stream (a NULL hipStream_t: the context's non-blocking
+    stream), so an accumulation could otherwise start before the fill."""
+    import torch
+    t = torch.zeros(*shape, dtype=dtype, device=device)
+    torch.cuda.synchronize()
+    return t
+
+
+def synced_zero_(t):
+    """t.zero_() completed before the next library call (see dev_zeros)."""
+    import torch
+    t.zero_()
+    torch.cuda.synchronize()
+    return t
+
+
 def strat_manifest():
     """Stratified crop sets of the deep configs (tests/golden/make_strat_golden.py)."""
     with open(os.path.join(GOLDEN, "strat_manifest.json")) as f:

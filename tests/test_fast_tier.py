@@ -22,7 +22,7 @@ import pytest
 import torch
 
 import openglraytracer_amd as rt
-from conftest import fixture_objects, load_fixture, load_strat, manifest, row_bands, strat_manifest
+from conftest import dev_zeros, fixture_objects, load_fixture, load_strat, manifest, row_bands, strat_manifest
 from oracle import port, scenes
 
 pytestmark = pytest.mark.gpu
@@ -168,14 +168,14 @@ def test_fast_tier_launch_shapes_agree(fast_ctx):
     sc = rt.Scene(fast_ctx, objs)
     try:
         singles = [rt.render(fast_ctx, sc, w, h, depth, view=v) for v in views]
-        batch = torch.zeros((3, h, w, 4), dtype=torch.float32, device="cuda")
+        batch = dev_zeros((3, h, w, 4), dtype=torch.float32, device="cuda")
         rt.render_batch(fast_ctx, sc, batch.data_ptr(), w, h, depth, views)
         torch.cuda.synchronize()
         for k in range(3):
             assert np.array_equal(batch[k].cpu().numpy(), singles[k])
         got = np.zeros_like(singles[0])
         for s in range(3):
-            buf = torch.zeros(rt.shard_rows(h, 8, 3, s) * w * 4, dtype=torch.float32, device="cuda")
+            buf = dev_zeros(rt.shard_rows(h, 8, 3, s) * w * 4, dtype=torch.float32, device="cuda")
             rt.render_shard(fast_ctx, sc, buf.data_ptr(), w, h, depth, 8, 3, s, view=views[0])
             torch.cuda.synchronize()
             got[frame.shard_row_ids(h, 8, 3, s)] = buf.cpu().numpy().reshape(-1, w, 4)

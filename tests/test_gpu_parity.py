@@ -17,7 +17,7 @@ import pytest
 import torch
 
 import openglraytracer_amd as rt
-from conftest import fixture_objects, load_fixture, manifest, parity_stats
+from conftest import dev_zeros, fixture_objects, load_fixture, manifest, parity_stats, synced_zero_
 from openglraytracer_amd import frame
 from oracle import port, scenes
 
@@ -144,7 +144,7 @@ def test_shards_reassemble_the_frame(gpu_ctx, n_shards, block):
     elems = frame.flat_shard_elems(1, h, w, block, n_shards)
     shards = []
     for s in range(n_shards):
-        buf = torch.zeros(elems, dtype=torch.float32, device="cuda")
+        buf = dev_zeros(elems, dtype=torch.float32, device="cuda")
         rt.render_shard(gpu_ctx, sc, buf.data_ptr(), w, h, 1, block, n_shards, s, view=view)
         shards.append(buf)
     torch.cuda.synchronize()
@@ -164,7 +164,7 @@ def test_batched_frames_equal_single_frames(gpu_ctx, n_shards):
     singles = [rt.render(gpu_ctx, sc, w, h, 1, view=v) for v in views]
     for shard in range(n_shards):
         rows = frame.shard_row_ids(h, block, n_shards, shard)
-        out = torch.zeros((len(views), len(rows), w, 4), dtype=torch.float32, device="cuda")
+        out = dev_zeros((len(views), len(rows), w, 4), dtype=torch.float32, device="cuda")
         rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, 1, views, block, n_shards, shard)
         got = out.cpu().numpy()
         for k in range(len(views)):
@@ -206,7 +206,7 @@ def test_host_frame_constants_equal_device_ones(gpu_ctx, case):
         got = {}
         for host in (True, False):
             gpu_ctx.set_host_frame_consts(host)
-            out = torch.zeros((2, h, w, 4), dtype=torch.float32, device="cuda")
+            out = dev_zeros((2, h, w, 4), dtype=torch.float32, device="cuda")
             rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, [view, other])
             got[host] = out.cpu().numpy()
             if not host:
@@ -229,7 +229,7 @@ def test_async_stream_equals_sync(gpu_ctx):
     sc = rt.Scene(gpu_ctx, objs)
     sync = rt.render(gpu_ctx, sc, 320, 180, 2, view=view)
     s = torch.cuda.Stream()
-    out = torch.zeros((180, 320, 4), dtype=torch.float32, device="cuda")
+    out = dev_zeros((180, 320, 4), dtype=torch.float32, device="cuda")
     with torch.cuda.stream(s):
         rt.render_device(gpu_ctx, sc, out.data_ptr(), 320, 180, 2, view=view, stream=s.cuda_stream)
     s.synchronize()
@@ -362,14 +362,14 @@ def test_monte_carlo_matches_oracle(gpu_ctx):
     w, h = 96, 54
     view = rt.make_view(None, 0.0)
     sc = rt.Scene(gpu_ctx, objs)
-    acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+    acc = dev_zeros((h, w, 4), dtype=torch.float32, device="cuda")
     rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, 1, 3, 0, seed=7, view=view)
     rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, 1, 2, 3, seed=7, view=view)
     o = port.render_accumulate(objs, w, h, 1, 3, 0, seed=7)
     o = port.render_accumulate(objs, w, h, 1, 2, 3, seed=7, accum=o)
     assert np.array_equal(acc.cpu().numpy(), o)
     # without jitter every sample is the reference frame
-    acc.zero_()
+    synced_zero_(acc)
     rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, 1, 3, 0, jitter=False, view=view)
     f = rt.render(gpu_ctx, sc, w, h, 1, view=view)
     assert np.array_equal(acc.cpu().numpy(), (f + f) + f)
@@ -486,11 +486,11 @@ def test_rgba8_surface_equals_packed_float_frame(gpu_ctx, cfg, w, h):
     assert np.array_equal(rt.render_rgba8(gpu_ctx, sc, w, h, depth, view=view, rows=(7, 40)), b[7:40])
     gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA8)
     try:
-        out = torch.zeros((2, h, w, 4), dtype=torch.uint8, device="cuda")
+        out = dev_zeros((2, h, w, 4), dtype=torch.uint8, device="cuda")
         rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, [view, view])
         got = out.cpu().numpy()
         assert np.array_equal(got[0], b) and np.array_equal(got[1], b)
-        acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+        acc = dev_zeros((h, w, 4), dtype=torch.float32, device="cuda")
         with pytest.raises(rt.RTError) as e:
             rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 1, view=view)
         assert e.value.code == rt.abi.RT_ERR_UNSUPPORTED
@@ -512,14 +512,14 @@ def test_rgb32f_exchange_format_equals_float_frames(gpu_ctx, n_shards):
     singles = [rt.render(gpu_ctx, sc, w, h, 0, view=v) for v in views]
     gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
     try:
-        one = torch.zeros((h, w, 3), dtype=torch.float32, device="cuda")
+        one = dev_zeros((h, w, 3), dtype=torch.float32, device="cuda")
         rt.render_device(gpu_ctx, sc, one.data_ptr(), w, h, 0, view=views[0])
         torch.cuda.synchronize()
         assert np.array_equal(one.cpu().numpy(), singles[0][..., :3])
         bufs = []
         for shard in range(n_shards):
             rows = frame.shard_row_ids(h, block, n_shards, shard)
-            out = torch.zeros((n_shards, len(rows), w, 3), dtype=torch.float32, device="cuda")
+            out = dev_zeros((n_shards, len(rows), w, 3), dtype=torch.float32, device="cuda")
             rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, 0, views, block, n_shards, shard)
             got = out.cpu().numpy()
             for k in range(n_shards):
@@ -568,7 +568,7 @@ def test_animated_frames_in_one_launch(gpu_ctx):
     w, h, depth = 96, 54, 2
     scs = [rt.Scene(gpu_ctx, rt.reference_objects(t)) for t in times]
     views = [rt.make_view(None, t) for t in times]
-    out = torch.zeros((len(times), h, w, 4), dtype=torch.float32, device="cuda")
+    out = dev_zeros((len(times), h, w, 4), dtype=torch.float32, device="cuda")
     rt.render_batch_scenes(gpu_ctx, scs, out.data_ptr(), w, h, depth, views)
     got = out.cpu().numpy()
     for k, t in enumerate(times):
@@ -635,10 +635,10 @@ def test_config5_monte_carlo_kernel_full_frame(gpu_ctx):
     view = rt.make_view(None, 0.0)
     sc = rt.Scene(gpu_ctx, objs)
     try:
-        acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+        acc = dev_zeros((h, w, 4), dtype=torch.float32, device="cuda")
         rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 0, seed=0, view=view)
         rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 2, seed=0, view=view)
-        one = torch.zeros_like(acc)
+        one = dev_zeros(acc.shape, dtype=acc.dtype)
         rt.render_accumulate(gpu_ctx, sc, one.data_ptr(), w, h, depth, 4, 0, seed=0, view=view)
         torch.cuda.synchronize()
         split, whole = acc.cpu().numpy(), one.cpu().numpy()
@@ -651,7 +651,7 @@ def test_config5_monte_carlo_kernel_full_frame(gpu_ctx):
             assert np.array_equal(whole[r0:r1], o1), (r0, parity_stats(whole[r0:r1], o1))
         # the two orders differ only by float re-association
         assert np.allclose(split, whole, rtol=1e-6, atol=1e-6)
-        one.zero_()
+        synced_zero_(one)
         rt.render_accumulate(gpu_ctx, sc, one.data_ptr(), w, h, depth, 2, 0, jitter=False, view=view)
         f = rt.render(gpu_ctx, sc, w, h, depth, view=view)
         assert np.array_equal(one.cpu().numpy(), f + f)
@@ -706,7 +706,7 @@ def test_multi_gpu_group_equals_single_frame(fmt, block):
             got = group.render(scs, w, h, depth, view=view, block_rows=block)
             assert np.array_equal(got, whole)
             dt = torch.uint8 if fmt == rt.abi.RT_OUTPUT_RGBA8 else torch.float32
-            dev = torch.zeros(whole.shape, dtype=dt, device="cuda")
+            dev = dev_zeros(whole.shape, dtype=dt, device="cuda")
             group.render_device(scs, dev.data_ptr(), w, h, depth, view=view, block_rows=block)
             assert np.array_equal(dev.cpu().numpy(), whole)
             k, g, a = group.last_ms()
@@ -957,7 +957,7 @@ def test_random_scenes_batch_shards_rgba8_and_mc(gpu_ctx, seed):
     sc = rt.Scene(gpu_ctx, objs, materials=mats, lights=lights)
     try:
         singles = [rt.render(gpu_ctx, sc, w, h, depth, view=v) for v in views]
-        batch = torch.zeros((3, h, w, 4), dtype=torch.float32, device="cuda")
+        batch = dev_zeros((3, h, w, 4), dtype=torch.float32, device="cuda")
         rt.render_batch(gpu_ctx, sc, batch.data_ptr(), w, h, depth, views)
         torch.cuda.synchronize()
         for k in range(3):
@@ -965,14 +965,14 @@ def test_random_scenes_batch_shards_rgba8_and_mc(gpu_ctx, seed):
         n = 3
         got = np.zeros_like(singles[0])
         for s in range(n):
-            buf = torch.zeros(rt.shard_rows(h, 4, n, s) * w * 4, dtype=torch.float32, device="cuda")
+            buf = dev_zeros(rt.shard_rows(h, 4, n, s) * w * 4, dtype=torch.float32, device="cuda")
             rt.render_shard(gpu_ctx, sc, buf.data_ptr(), w, h, depth, 4, n, s, view=views[0])
             torch.cuda.synchronize()
             got[frame.shard_row_ids(h, 4, n, s)] = buf.cpu().numpy().reshape(-1, w, 4)
         assert np.array_equal(got, singles[0], equal_nan=True), seed
         assert np.array_equal(rt.render_rgba8(gpu_ctx, sc, w, h, depth, view=views[0]), rt.pack_rgba8(singles[0]))
         if depth <= 2:
-            acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+            acc = dev_zeros((h, w, 4), dtype=torch.float32, device="cuda")
             rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 0, seed=seed, view=views[0])
             rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, depth, 2, 2, seed=seed, view=views[0])
             torch.cuda.synchronize()

@@ -13,7 +13,12 @@ step() {  # name timeout cmd... ; stops the session on any failure
   timeout -k 10 $t "$@" > $out/$name.log 2>&1
   local rc=$?
   echo "   rc=$rc"; tail -3 $out/$name.log
-  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  if [ $rc -ne 0 ]; then
+    # SOFT_TESTS=1: a failing test run (rc 1, pytest's "tests failed") does
+    # not stop the session; any other status (timeout, abort, fault) does
+    if [ "${SOFT_TESTS:-0}" = 1 ] && [ "$name" = gpu_tests ] && [ $rc -eq 1 ]; then echo "   (tests failed; continuing)"; return 0; fi
+    echo "STOP after $name (rc=$rc)"; exit $rc
+  fi
 }
 if want list; then step counters 60 rocprofv3 -L; fi
 if want tests; then step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread; fi
@@ -34,6 +39,7 @@ fi
 if want prof5; then
   step prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
 fi
+if want phase; then step phase 300 env PHASE_DUMP=gpurun_out/$tag/phase.npz python tools/phase_trace.py config2 phase; fi
 if want shards; then step shard_timing 600 python tools/shard_timing.py; fi
 if want cycles; then step cycles 300 python tools/cycles.py cycles config2 config3 config4; fi
 if want stats; then step stats 300 python tools/stats.py stats config2 config3 config4; fi

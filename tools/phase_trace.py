@@ -116,3 +116,45 @@ w = np.arange(waves) % 4
 for k in range(4):
     m = w == k
     print("  wave %d of its group: setup done %.2f, barrier left %.2f (from entry)" % (k, (P[m, 2] - T[m, 0]).mean(), (P[m, 3] - T[m, 0]).mean()))
+
+# ---- work-group order and the launch's tail (round 4) -------------------
+# Per work-group duration (first wave start to last wave end) by tile, and a
+# list-scheduling replay of the 8 x 256 work-group slots (8 resident per CU)
+# with the measured durations in three dispatch orders: the hardware's
+# (blockIdx: row-major tiles), a static centre-out order, and longest first
+# (the bound a perfect cost predictor would reach). A permuted order only
+# pays if the measured durations are predictable from the tile position.
+import heapq  # noqa: E402
+
+_, W0, H0, _ = scenes.CONFIGS[cfg]
+gx, gy = (W0 + 15) // 16, (H0 + 15) // 16
+wg_start = start.reshape(-1, 4).min(1)
+wg_end = end.reshape(-1, 4).max(1)
+wg_dur = wg_end - wg_start
+slots = 8 * 256
+
+
+def replay(order):
+    heap = [0.0] * slots
+    last = 0.0
+    for k in order:
+        t = heapq.heappop(heap) + wg_dur[k]
+        last = max(last, t)
+        heapq.heappush(heap, t)
+    return last
+
+
+ty, tx = np.divmod(np.arange(gx * gy), gx)
+centre = np.argsort(np.hypot((tx + 0.5) / gx - 0.5, ((ty + 0.5) / gy - 0.5) * gy / gx), kind="stable")
+print("work-groups %d, duration mean %.2f us p10 %.2f p90 %.2f; measured last end %.2f us" %
+      (gx * gy, wg_dur.mean(), np.percentile(wg_dur, 10), np.percentile(wg_dur, 90), span))
+print("replay (us): ideal %.2f  blockIdx order %.2f  centre-out %.2f  longest-first %.2f" %
+      (wg_dur.sum() / slots, replay(np.arange(gx * gy)), replay(centre), replay(np.argsort(-wg_dur, kind="stable"))))
+rows = wg_dur.reshape(gy, gx)
+print("mean work-group duration by tile-row band (top to bottom, 8 bands):",
+      " ".join("%.2f" % b.mean() for b in np.array_split(rows, 8, axis=0)))
+print("mean work-group duration by tile-column band (8 bands):",
+      " ".join("%.2f" % b.mean() for b in np.array_split(rows, 8, axis=1)))
+dump = os.environ.get("PHASE_DUMP")
+if dump:
+    np.savez_compressed(dump, start=start, end=end, gx=gx, gy=gy)
