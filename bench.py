@@ -112,11 +112,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0,
                     help="approximate budget of the llvmpipe baseline samples")
-    ap.add_argument("--precision", choices=["exact", "fast"], default="exact",
-                    help="the timed tier: exact (default, bit-identical to the reference's GL render) or fast "
-                         "(RT_PRECISION_FAST: within 1e-5 per channel, depth >= 1 only)")
-    ap.add_argument("--no-fast-tier", action="store_true",
-                    help="config3/config4 at N=1: skip the secondary RT_PRECISION_FAST measurement")
     ap.add_argument("--no-rgba8", action="store_true",
                     help="config2 at N=1: skip the same-surface (GL_RGBA8) measurement")
     ap.add_argument("--no-single-frame", action="store_true",
@@ -258,8 +253,6 @@ def main():
     ctx = rt.Context(device)
     scene = rt.Scene(ctx, rt.bench_objects(cfg["spheres"], 0))
     ctx.set_timing(False)  # no per-launch markers of the library's own
-    tiers = {"exact": rt.abi.RT_PRECISION_EXACT, "fast": rt.abi.RT_PRECISION_FAST}
-    ctx.set_precision(tiers[args.precision])
     # Streams of our own: renders are launched asynchronously on `render_s`
     # (the C-ABI treats a NULL stream — torch's default stream handle is 0 —
     # as "synchronous on the context's stream", like glFinish); the current
@@ -578,22 +571,6 @@ def main():
         extra["single_frame"] = {"frames_per_launch": 1, "us_per_frame": round(us, 3),
                                  "value": round(W * H / us, 3), "unit": "Mrays/s",
                                  "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
-    if (not batched and not mc and world == 1 and DEPTH >= 1 and args.precision == "exact"
-            and not args.no_fast_tier):
-        # the same frame in the tolerance tier (RT_PRECISION_FAST: the same
-        # rays, the recursion's colours accumulated forward; within 1e-5 per
-        # channel of the reference, tests/test_fast_tier.py)
-        ctx.set_precision(rt.abi.RT_PRECISION_FAST)
-        pf = frame_plan()
-        ef, kf, _ = measure(pf, args.steps, args.warmup)
-        extra["fast_tier"] = {
-            "precision": "RT_PRECISION_FAST (within 1e-5 per channel of the GL render; the default line is "
-                         "bit-identical)",
-            "value": round(pf.rays_per_step * args.steps / ef / 1e6, 3), "unit": "Mrays/s",
-            "ms_per_step": round(ef / args.steps * 1e3, 5), "kernel_ms": round(kf, 5),
-            "roofline_frac": round(pf.px_per_launch * pf.bytes_per_pixel / (kf * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
-        ctx.set_precision(rt.abi.RT_PRECISION_EXACT)
-        del pf
     if batched and world == 1 and rank == 0 and not args.no_rgba8:
         # the same F frames into the GL_RGBA8 surface the row-tiled N>1
         # steps write (main.cpp:223): the same-surface point of the 1..8-GPU
@@ -617,8 +594,7 @@ def main():
     achieved_f4 = plan.px_per_launch * 16 / (avg_kernel_ms * 1e-3) / 1e9
     fpl = plan.px_per_launch // (W * H) if batched and world == 1 else 1
     build = rt.lib().rt_version().decode()
-    # (the fast tier's kernels have their own profiles: pmc_<workload>_fast_latest.json)
-    pmc = pmc_latest(wl + ("_fast" if args.precision == "fast" else ""), fpl, build) if world == 1 else {}
+    pmc = pmc_latest(wl, fpl, build) if world == 1 else {}
     traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
         cpu = None
@@ -673,7 +649,6 @@ def main():
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "precision": args.precision,
             "data": "synthetic (seeded scene, SURVEY.md §8(d) %s)" % wl,
             "config": workload,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

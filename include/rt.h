@@ -301,16 +301,9 @@ int rt_multi_last_ms(rt_multi *m, float *kernel_ms, float *gather_ms, float *ass
  * 16 spheres + 1 box);
  * 0: every work-group derives them on the device. Output is identical. */
 #define RT_OPT_FRAME_CONSTS 4
-/* RT_OPT_PRECISION (default RT_PRECISION_EXACT): RT_PRECISION_EXACT renders
- * every pixel bit-identical to the reference's GL render (llvmpipe) of the
- * same frame. RT_PRECISION_FAST is the tolerance tier: the same rays, with
- * the recursion's colours accumulated forward (weights down the ray tree
- * instead of nested mix() on the way back up, raytrace_compute.glsl:
- * 1034-1054), within north_star's 1e-5 per channel of the reference on every
- * GL fixture; it changes only max_depth >= 1 renders. */
-#define RT_OPT_PRECISION 6
-#define RT_PRECISION_EXACT 0
-#define RT_PRECISION_FAST 1
+/* (option 6, a tolerance tier that summed the recursion's colours forward
+ * instead of mixing them on the way back up, measured even with the exact
+ * walk and was removed: DESIGN.md §3.) */
 /* (option 5, a level-by-level wavefront path for deep trees, was measured
  * 2x slower than the depth-first walk and removed: DESIGN.md §3.) */
 int rt_context_set(rt_context *ctx, int option, int value);

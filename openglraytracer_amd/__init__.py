@@ -222,13 +222,6 @@ class Context:
         (default), else derived by every work-group (output identical)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_FRAME_CONSTS, 1 if on else 0))
 
-    def set_precision(self, tier):
-        """RT_OPT_PRECISION: abi.RT_PRECISION_EXACT (default: bit-identical to
-        the reference's GL render) or abi.RT_PRECISION_FAST (the tolerance
-        tier: forward-accumulated recursion colours, within 1e-5 per channel;
-        depth >= 1 only)."""
-        _check(lib().rt_context_set(self._h, abi.RT_OPT_PRECISION, tier))
-
     def set_output(self, fmt):
         """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel),
         abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)

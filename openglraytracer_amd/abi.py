@@ -22,9 +22,6 @@ RT_OPT_CULLING = 1
 RT_OPT_TIMING = 2
 RT_OPT_OUTPUT = 3
 RT_OPT_FRAME_CONSTS = 4
-RT_OPT_PRECISION = 6
-RT_PRECISION_EXACT = 0
-RT_PRECISION_FAST = 1
 RT_OUTPUT_RGBA32F = 0
 RT_OUTPUT_RGBA8 = 1
 RT_OUTPUT_RGB32F = 2

@@ -195,7 +195,6 @@ struct LaunchParams {
     // Rows [slice_begin, slice_begin + slice_rows) of the launch's local rows
     // (the whole launch when slice_rows = 0).
     int32_t slice_begin, slice_rows;
-    int32_t precision;  // RT_PRECISION_*: the exact kernels or the tolerance tier
     float4 frame_consts[kMaxFrameConsts];
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
@@ -268,7 +267,6 @@ struct rt_context {
     int timing = 1;   // RT_OPT_TIMING
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int host_consts = 1;  // RT_OPT_FRAME_CONSTS
-    int precision = 0;    // RT_OPT_PRECISION
     int n_cu = 0;               // compute units of the device
     int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
     unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots

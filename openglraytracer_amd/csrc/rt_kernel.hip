@@ -1352,87 +1352,6 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
     }
 }
 
-// The tolerance tier's walk (RT_PRECISION_FAST, depth >= 1): the same rays in
-// the same order as trace_tree, with the colour accumulated forward. A node's
-// value mix(mix(phong, R, rho), T, tau) (each mix only for a spawned child) is
-// the weighted sum (1-rho')(1-tau') phong + rho'(1-tau') R + tau' T with
-// rho' = rho for a spawned reflection child, else 0 (tau' likewise), so the
-// pixel is the sum over its tree of weight x phong, a child's weight being its
-// parent's times rho'(1-tau') (reflection) or tau' (refraction). Nothing
-// waits for a subtree: only a node with BOTH children keeps a record — its
-// pending refraction ray and weight, 32 B — where trace_tree keeps a 40-B frame
-// for every node with children and reloads it on every return
-// (tools/model/walk_model.py, config 4: 10.1 instead of 29.9 frame rounds per
-// wave tile, 193 instead of 901 B of frame traffic per pixel). The rays are
-// bit-identical to trace_tree's; the colour differs by the rounding of a sum
-// instead of nested mixes (|d| <= 1e-5 per channel against every GL fixture,
-// tests/test_gpu_parity.py::test_fast_tier_*).
-struct Pending {
-    float4 rs_w;       // pending refraction ray start, its weight
-    float4 rd_level;   // its direction, its level (int bits)
-};
-template <int kDepth, class Emit>
-__device__ __forceinline__ void trace_tree_linear(const Scene &S, Ray ray, bool active, Emit &&emit) {
-    Pending stack[kDepth];
-    int sp = 0;
-    int level = 0;
-    float w = 1.0f;
-    v3 acc = mk(0.0f, 0.0f, 0.0f);
-    bool done = !active;
-    bool first = true;
-    while (__any(!done)) {
-        const bool valid = !done;
-        const bool primary = first;
-        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
-        first = false;
-        const bool hit = valid && h.obj >= 0;
-        const Collision c = primary ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
-        const v3 col = phong(S, ray, c, hit);
-        if (!valid) continue;
-        const MatRec &m = S.mat[c.material];
-        const bool sr = hit && level < kDepth && m.reflectivity > 0.0f;
-        const bool st = hit && level < kDepth && m.transparency > 0.0f;
-        const float rho = sr ? m.reflectivity : 0.0f, tau = st ? m.transparency : 0.0f;
-        const float keep = 1.0f - tau;
-        if (hit) acc = add(acc, muls(col, w * ((1.0f - rho) * keep)));  // a missed ray is black
-        if (sr || st) {
-            v3 rd = ray.dir;
-            if (__any(st)) {
-                const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
-                rd = refract(ray.dir, c.n, ratio);
-            }
-            const v3 rs = sub(c.p, muls(c.n, 0.001f));
-            if (sr && st) {  // the refraction child waits
-                stack[sp] = {make_float4(rs.x, rs.y, rs.z, w * tau),
-                             make_float4(rd.x, rd.y, rd.z, __int_as_float(level + 1))};
-                ++sp;
-            }
-            if (sr) {
-                ray.start = add(c.p, muls(c.n, 0.001f));
-                ray.dir = reflect(ray.dir, c.n);
-                w = w * (rho * keep);
-            } else {
-                ray.start = rs;
-                ray.dir = rd;
-                w = w * tau;
-            }
-            ++level;
-            continue;
-        }
-        if (sp > 0) {  // the deepest pending refraction child next
-            --sp;
-            const Pending q = stack[sp];
-            ray.start = mk(q.rs_w.x, q.rs_w.y, q.rs_w.z);
-            ray.dir = mk(q.rd_level.x, q.rd_level.y, q.rd_level.z);
-            w = q.rs_w.w;
-            level = __float_as_int(q.rd_level.w);
-            continue;
-        }
-        emit(acc);
-        done = true;
-    }
-}
-
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     if (p.n_shards <= 0) return p.row_begin + local;
     const int blk = local / p.block_rows;
@@ -1634,7 +1553,7 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
 // One 8x8 wave tile (wx, wy) of view z: lane l renders pixel (8 wx + l % 8,
 // 8 wy + l / 8). `pre`: the lane's camera ray, already computed (the tiled
 // path computes it while the scene is staged), or nullptr.
-template <int kDepth, bool kAccum, bool kFast>
+template <int kDepth, bool kAccum>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
@@ -1665,10 +1584,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 #else
         if constexpr (kDepth > 0) {
             // each lane's pixel stored as soon as its tree is finished
-            if constexpr (kFast)
-                trace_tree_linear<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
-            else
-                trace_tree<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
+            trace_tree<kDepth>(S, ray, active, [&](v3 col) { store_pixel(p, z, idx, col); });
             return;
         }
         const v3 col = trace0(S, ray, active);
@@ -1684,10 +1600,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
             const float jy = p.jitter ? jitter_u(p.seed, sid, pixel, 1u) : 0.0f;
             v3 col = mk(0.0f, 0.0f, 0.0f);
             if constexpr (kDepth == 0) col = trace0(S, camera_ray(p, V, x, y, jx, jy), active);
-            else if constexpr (kFast)
-                trace_tree_linear<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active, [&](v3 c) { col = c; });
-            else
-                trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active, [&](v3 c) { col = c; });
+            else trace_tree<kDepth>(S, camera_ray(p, V, x, y, jx, jy), active, [&](v3 c) { col = c; });
             acc = add(acc, col);
         }
         if (active) {
@@ -1721,7 +1634,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 // 52 -> 67 us, 8-frame launches, tiled either way, 41.5 -> 50.6 us per frame)
 constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 
-template <int kDepth, bool kAccum, bool kFast>
+template <int kDepth, bool kAccum>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     const bool queued = kQueuedDepth(kDepth) && p.sched != nullptr;
@@ -1827,7 +1740,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
         int nxt = 0;
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
         const int wx = queued ? t % wtx : own_wx, wy = queued ? t / wtx : own_wy;
-        render_wave_tile<kDepth, kAccum, kFast>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
+        render_wave_tile<kDepth, kAccum>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
                                               own_ray, !(queued || kAccum));
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
@@ -1868,10 +1781,10 @@ int groups_per_cu(const void *fn, size_t lds) {
     return n;
 }
 
-template <int kDepth, bool kAccum, bool kFast>
+template <int kDepth, bool kAccum>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
-    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum, kFast>);
+    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
     dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, p.n_views);
     const int wave_tiles = ((p.width + 7) / 8) * ((p.slice_rows + 7) / 8);
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
@@ -1883,19 +1796,13 @@ hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     } else {
         p.sched = nullptr;
     }
-    hipLaunchKernelGGL((render_kernel<kDepth, kAccum, kFast>), grid, dim3(kThreads), lds, stream, p);
+    hipLaunchKernelGGL((render_kernel<kDepth, kAccum>), grid, dim3(kThreads), lds, stream, p);
     return hipGetLastError();
 }
 
 template <int kDepth>
 hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
-    // the tolerance tier (RT_PRECISION_FAST) differs from the exact kernels
-    // only where a ray tree is walked (trace_tree_linear, depth >= 1)
-    if constexpr (kDepth >= 1) {
-        if (p.precision == RT_PRECISION_FAST)
-            return p.spp > 0 ? launch_kernel<kDepth, true, true>(p, stream) : launch_kernel<kDepth, false, true>(p, stream);
-    }
-    return p.spp > 0 ? launch_kernel<kDepth, true, false>(p, stream) : launch_kernel<kDepth, false, false>(p, stream);
+    return p.spp > 0 ? launch_kernel<kDepth, true>(p, stream) : launch_kernel<kDepth, false>(p, stream);
 }
 
 }  // namespace
@@ -1966,12 +1873,10 @@ int check_kernarg_block(hipStream_t stream) {
 // (gfx950 has 160 KiB per CU). Best effort: a failure only lowers the largest
 // scene that fits, which rt_scene_create checks.
 hipError_t allow_large_lds(size_t bytes) {
-#define RT_KFN(d, f) reinterpret_cast<const void *>(&render_kernel<d, false, f>), \
-                     reinterpret_cast<const void *>(&render_kernel<d, true, f>)
-#define RT_KFN2(d) RT_KFN(d, false), RT_KFN(d, true)
-    const void *fns[] = {RT_KFN(0, false), RT_KFN2(1), RT_KFN2(2), RT_KFN2(3), RT_KFN2(4),
-                         RT_KFN2(5), RT_KFN2(6), RT_KFN2(7), RT_KFN2(8), RT_KFN2(9)};
-#undef RT_KFN2
+#define RT_KFN(d) reinterpret_cast<const void *>(&render_kernel<d, false>), \
+                  reinterpret_cast<const void *>(&render_kernel<d, true>)
+    const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
+                         RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9)};
 #undef RT_KFN
     for (const void *f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
@@ -2014,7 +1919,7 @@ extern "C" int rt_debug_phase_read(void *dst, size_t bytes) {
 }
 extern "C" int rt_debug_occupancy(size_t lds) {
     int n = -1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&rtamd::render_kernel<0, false, false>),
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void *>(&rtamd::render_kernel<0, false>),
                                                      rtamd::kThreads, lds) != hipSuccess)
         return -1;
     return n;

@@ -32,6 +32,14 @@ iteration by iteration under two frame schemes:
 Prints per scheme: wave iterations, store rounds, load rounds and bytes per
 wave tile, so a calibrated cost per round (from an ablation build that keeps
 no frames) predicts the time of each scheme.
+
+Outcome (round 4): config 4 exact 29.9 frame rounds / 901 B per pixel,
+linear 10.1 / 193; calibrated on the r02l no-frames ablation (-31 %), the
+linear walk was predicted at about -20 %. Built (RT_PRECISION_FAST, within
+4.8e-7 of every GL fixture) and measured EVEN: config 4 14.67 vs 14.69 ms,
+config 3 0.873 vs 0.895 ms (profiles/r04b_ab_fast_tier_config34.log). The
+frame rounds are not on the critical path; the ablation's gain came from the
+different (wrong) rays it traced. The variant was removed from the product.
 """
 import argparse
 import json
