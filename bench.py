@@ -16,21 +16,24 @@ tail). The total work of a step is fixed: strong scaling.
     N>1 steps write, so the N=1 and N>1 points share a surface; every line's
     roofline also carries `frac_float4_equivalent` (the pixels at 16 B).
   * N>1 (north_star: "image row-tiles shard across the GPUs with an RCCL
-    gather over xGMI to assemble the frame"): every frame is row-tiled over
-    the N ranks in interleaved 8-row blocks; each rank renders its blocks of
-    all F frames (rt_render_batch with shards), one RCCL gather per step
-    brings the shards to rank 0, which de-interleaves them into the F frames;
-    the gather of step i overlaps the render of step i+1 (double-buffered).
-    The kernel writes the shipped app's GL_RGBA8 surface format
-    (main.cpp:152-159, :223; RT_OUTPUT_RGBA8, byte-exact vs the reference's
-    GL render), and the shards travel without its alpha byte, which is always
-    0 (:404): 3 B per pixel instead of 16 — 6.2 MB per 1080p frame through
-    rank 0's xGMI ingress — into one contiguous buffer that a single
-    index_select de-interleaves. The line also carries `independent_frames`: every
-    rank renders F whole frames of its own with no collective (weak scaling),
-    and `verified`: the assembled frames of the last step equal rank 0's own
-    whole-frame render byte for byte. --frame-exchange all_to_all instead
-    hands frame k to rank k (N gathers at once); none = independent frames.
+    gather over xGMI to assemble the frame"): every frame of the step is
+    row-tiled over the N ranks in interleaved 8-row blocks; each rank renders
+    its blocks of all F frames (rt_render_batch with shards) into the shipped
+    app's GL_RGBA8 surface format (main.cpp:152-159, :223; RT_OUTPUT_RGBA8,
+    byte-exact vs the reference's GL render), and the shards travel without
+    its alpha byte, which is always 0 (:404): 3 B per pixel. The default
+    exchange (--frame-exchange spread) assembles frame k on rank k % N with
+    one RCCL all-to-all per step: each frame is still gathered from all N
+    row-tiles, but the step's bytes enter through every rank's xGMI links
+    instead of rank 0's alone (xGMI is point-to-point; DESIGN.md §6 predicts
+    the gather-to-rank-0 shape link-bound at every N). --frame-exchange
+    gather brings every frame to rank 0 (one contiguous buffer, one
+    index_select); all_to_all keeps F frames per rank in flight (weak
+    scaling); none = independent whole frames. The exchange of step i
+    overlaps the render of step i+1 (double-buffered). The line also carries
+    `independent_frames` (every rank renders F whole frames of its own, no
+    collective) and `verified`: the assembled frames of the last step equal
+    the assembling rank's own whole-frame render byte for byte.
 
 config3 / config4 (3840x2160 / 64 spheres / depth 2, and
 7680x4320 / 256 spheres / depth 4 row-tiled across the GPUs with an RCCL
@@ -97,10 +100,12 @@ def parse():
     ap.add_argument("--frames", type=int, default=8,
                     help="config2: animated frames per step, up to 8 per launch (rt_render_batch; "
                          "SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
-    ap.add_argument("--frame-exchange", choices=["gather", "all_to_all", "none"], default="gather",
-                    help="config2 at N>1: gather = every frame row-tiled over the ranks and gathered to rank 0 "
-                         "(north_star); all_to_all = frame k gathered to rank k; none = every rank renders "
-                         "whole frames of its own")
+    ap.add_argument("--frame-exchange", choices=["spread", "gather", "all_to_all", "none"], default="spread",
+                    help="config2 at N>1: spread (default) = every frame of the step row-tiled over the ranks, "
+                         "frame k assembled on rank k %% N by one all-to-all (rank 0's xGMI ingress 1/N of the "
+                         "step); gather = every frame gathered to rank 0; all_to_all = F frames per rank in "
+                         "flight, frame k gathered to rank k (weak scaling); none = every rank renders whole "
+                         "frames of its own")
     ap.add_argument("--surface", choices=["auto", "rgba32f", "rgba8"], default="auto",
                     help="config2 surface: auto = float4 at N=1, the GL_RGBA8 surface for row-tiled frames at N>1")
     ap.add_argument("--no-independent", action="store_true",
@@ -293,6 +298,8 @@ def main():
                     rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * H * W * ch, W, H, DEPTH, vs, stream=sh)
             return Plan(bufs, render, world * F * W * H, W * H * F // len(chunks), esize * ch, len(chunks),
                         per_launch=False)
+        if mode == "spread":
+            return spread_plan()
         n_frames = F if mode == "gather" else world * F
         views = [rt.make_view(None, frame_time(k)) for k in range(n_frames)]
         rows_mine = rt.shard_rows(H, BLOCK_ROWS, world, rank)
@@ -353,6 +360,39 @@ def main():
                 return frame.assemble_frames(recv[slot], F, H, W, BLOCK_ROWS, world, channels=ch, idx=idx)
         return Plan(bufs, render, n_frames * W * H, W * rows_mine * n_frames // len(chunks), esize * ch,
                     len(chunks), collective, assemble)
+
+    def spread_plan():
+        """config2 at N>1, --frame-exchange spread (the default): the step's F
+        frames row-tiled over all ranks, frame k assembled on rank k % N by
+        one all-to-all of RGB8 shards; rank r renders its row blocks of all F
+        frames, grouped by destination (frame.spread_plan)."""
+        surface("rgba8")
+        order, ins, outs, mine = frame.spread_plan(H, W, BLOCK_ROWS, world, rank, F, channels=3)
+        views = [rt.make_view(None, frame_time(k)) for k in order]
+        rows_mine = rt.shard_rows(H, BLOCK_ROWS, world, rank)
+        frame_elems = rows_mine * W
+        bufs = [torch.zeros(F * frame_elems, dtype=torch.int32, device="cuda") for _ in range(2)]
+        sends = [torch.empty(F * frame_elems * 3, dtype=torch.uint8, device=coll_dev) for _ in bufs]
+        recvs = [torch.empty(sum(outs), dtype=torch.uint8, device=coll_dev) for _ in bufs]
+        idx = torch.as_tensor(frame.assembly_rows(H, BLOCK_ROWS, world, len(mine)), device=coll_dev)
+        chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, F, rt.abi.RT_MAX_BATCH)]
+
+        def render(buf):
+            for j, vs in chunks:
+                rt.render_batch(ctx, scene, buf.data_ptr() + 4 * j * frame_elems, W, H, DEPTH, vs,
+                                BLOCK_ROWS, world, rank, stream=sh)
+
+        def collective(slot, src):
+            frame.pack_rgb8(src, sends[slot])
+            dist.all_to_all_single(recvs[slot], sends[slot], outs, ins)  # RCCL: frame k -> rank k % N
+
+        def assemble(slot):
+            if not mine:
+                return None
+            return frame.assemble_frames(recvs[slot], len(mine), H, W, BLOCK_ROWS, world, channels=3, idx=idx)
+        plan = Plan(bufs, render, F * W * H, frame_elems * F // len(chunks), 4, len(chunks), collective, assemble)
+        plan.mine = mine
+        return plan
 
     def frame_plan():
         """config3 / config4: one frame per step, whole at N=1, row-tiled +
@@ -518,6 +558,8 @@ def main():
     if batched:
         mode = args.frame_exchange if world > 1 else "none"
         surf = args.surface if args.surface != "auto" else ("rgba8" if world > 1 and mode != "none" else "rgba32f")
+        if mode == "spread":
+            surf = "rgba8"  # (the exchange packs GL_RGBA8 texels to RGB8)
         plan = batch_plan(mode, surf)
     elif mc:
         view = rt.make_view(None, 0.0)
@@ -534,6 +576,9 @@ def main():
     if world > 1 and not args.no_verify and not mc:
         if batched and mode == "gather":
             verified = verify(plan, F, [frame_time(k) for k in range(F)], surfaces[surf][1], surfaces[surf][2])
+        elif batched and mode == "spread":
+            verified = verify(plan, len(plan.mine), [frame_time(k) for k in plan.mine], surfaces["rgba8"][1],
+                              surfaces["rgba8"][2])
         elif batched and mode == "all_to_all":
             verified = verify(plan, F, [frame_time(rank * F + k) for k in range(F)], surfaces[surf][1],
                               surfaces[surf][2])
@@ -608,6 +653,15 @@ def main():
                              "parallelism": ("whole frames x%d (rank r renders frames [rF, (r+1)F) of the "
                                              "animated loop), no collective" % world) if world > 1
                                             else "single GPU"})
+        elif batched and mode == "spread":
+            collective = "all_to_all_single (frame k of the step to rank k % N; RGB8 shards)"
+            workload.update({"frames_per_step": F, "frames_per_launch": min(F, rt.abi.RT_MAX_BATCH),
+                             "row_block": BLOCK_ROWS,
+                             "output": "GL_RGBA8 surface (4 B per pixel) shards, sent as RGB8 (the constant "
+                                       "alpha byte dropped); frame k assembled on rank k % N",
+                             "parallelism": "every frame row-tiled x%d in interleaved %d-row blocks + one RCCL "
+                                            "all-to-all per step assembling frame k on rank k %% %d, overlapped "
+                                            "with the next render" % (world, BLOCK_ROWS, world)})
         elif batched and mode == "gather":
             collective = "gather to rank 0 (one per step: the shards of all F frames)"
             workload.update({"frames_per_step": F, "frames_per_launch": min(F, rt.abi.RT_MAX_BATCH),
@@ -636,7 +690,7 @@ def main():
                              "float3 shards (alpha 0 dropped) gathered to rank 0, de-interleaved there",
                              "parallelism": ("interleaved 8-row blocks x%d + RCCL gather to rank 0, overlapped "
                                              "with the next render" % world) if world > 1 else "single GPU"})
-        strong = not (batched and world > 1 and mode in ("none", "all_to_all"))
+        strong = not (batched and world > 1 and mode in ("none", "all_to_all"))  # (spread, gather: F frames per step)
         line = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -60,6 +60,18 @@ __device__ __forceinline__ v3 sel(bool c, v3 a, v3 b) { return {c ? a.x : b.x, c
 // dot(vec3) as llvmpipe associates it: x + (y + z)
 __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
 
+// Price-of-exactness ablation (timing and accuracy probes, never the product
+// build: tools/ab.py, tools/ab_accuracy.py): RT_FAST_DIV (a * v_rcp(b) for
+// every division), RT_FAST_RSQ (v_rsq in normalize), RT_FAST_SQRT (v_sqrt in
+// the sphere tests and refract), RT_FAST_POW (v_log / v_exp in the specular
+// pow); RT_FAST_MATH sets all four.
+#ifdef RT_FAST_MATH
+#define RT_FAST_DIV
+#define RT_FAST_RSQ
+#define RT_FAST_SQRT
+#define RT_FAST_POW
+#endif
+
 // ---- correctly rounded division and square root, short forms -------------
 // hipcc lowers a / b (IEEE) to div_scale(b), rcp, 2 fma (the refined
 // reciprocal r), div_scale(a), mul, 3 fma, div_fmas, div_fixup; and sqrtf(x)
@@ -89,7 +101,7 @@ __device__ __forceinline__ Rcp rcp_refined(float b) {
     return {b, r};
 }
 __device__ __forceinline__ float div_r(float a, Rcp d) {
-#ifdef RT_FAST_MATH
+#ifdef RT_FAST_DIV
     return a * __builtin_amdgcn_rcpf(d.b);
 #endif
     const float q = a * d.r;
@@ -101,9 +113,9 @@ __device__ __forceinline__ float sqrt_short(float x) {
     const float r = __builtin_fmaf(-dn, s, x) <= 0.0f ? dn : s;
     return __builtin_fmaf(-up, s, x) > 0.0f ? up : r;
 }
-// a / b: the IEEE division (RT_FAST_MATH ablation builds: a * v_rcp(b))
+// a / b: the IEEE division (RT_FAST_DIV ablation builds: a * v_rcp(b))
 __device__ __forceinline__ float fdiv(float a, float b) {
-#ifdef RT_FAST_MATH
+#ifdef RT_FAST_DIV
     return a * __builtin_amdgcn_rcpf(b);
 #else
     return a / b;
@@ -112,7 +124,7 @@ __device__ __forceinline__ float fdiv(float a, float b) {
 // 1 / sqrt(d), both correctly rounded (GLSL inversesqrt as llvmpipe evaluates
 // it): the refined reciprocal of the short square root
 __device__ __forceinline__ float inv_sqrt(float d) {
-#ifdef RT_FAST_MATH
+#ifdef RT_FAST_RSQ
     return __builtin_amdgcn_rsqf(d);
 #endif
     if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return rcp_refined(sqrt_short(d)).r;
@@ -141,7 +153,7 @@ __device__ __forceinline__ float inv_sqrt_near_one(float d) {
 // is within 2048 ulps of 1, else the general path; bit-identical either way
 __device__ __forceinline__ v3 normalize_unit(v3 a) {
     const float d = dot(a, a);
-#ifdef RT_FAST_MATH
+#ifdef RT_FAST_RSQ
     return muls(a, __builtin_amdgcn_rsqf(d));
 #endif
     if (__all(near_one(d))) return muls(a, inv_sqrt_near_one(d));
@@ -210,7 +222,7 @@ __device__ __forceinline__ float glsl_pow(float x, float y) { return glsl_exp2(g
 // vectors is at most about 3 or NaN, so glsl_log2's NaN and +inf cases are
 // never reached; its zero case becomes a select
 __device__ __forceinline__ float glsl_pow_cos(float x, float y) {
-#ifdef RT_FAST_MATH
+#ifdef RT_FAST_POW
     return x == 0.0f ? 0.0f : __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
 #endif
     const uint32_t i = __float_as_uint(x);
@@ -504,7 +516,7 @@ __device__ __forceinline__ float root_floor(float qa2) {
 // active lane's operand is in its range (qd >= 2^-96; +inf included), else
 // the IEEE sequence (config 4 18.20 -> 17.94 ms, config 3 1.030 -> 1.001 ms)
 __device__ __forceinline__ float sphere_sqrt(float qd) {
-#ifdef RT_FAST_MATH
+#ifdef RT_FAST_SQRT
     return __builtin_amdgcn_sqrtf(qd);
 #endif
     if (__all(qd >= 0x1p-96f)) return sqrt_short(qd);

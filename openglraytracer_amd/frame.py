@@ -12,7 +12,9 @@ Two assemblies:
   rank k — N gathers at once, i.e. one all-to-all in which every rank sends
   frame k's rows to rank k — so each xGMI link carries 1/N of the traffic a
   single root would pull through its own links — `exchange_splits` +
-  `assemble_frame`.
+  `assemble_frame`;
+* spread: the same exchange for a fixed step of F frames (frame k assembled
+  on rank k % N) — `spread_plan` + `assemble_frames`.
 
 Pure index bookkeeping (numpy / torch tensors); no rendering here.
 """
@@ -114,6 +116,29 @@ def exchange_splits(height, width, block_rows, n_shards, rank, channels=4, frame
     rows = [len(shard_row_ids(height, block_rows, n_shards, s)) for s in range(n_shards)]
     f = frames_per_rank
     return [f * rows[rank] * width * channels] * n_shards, [f * r * width * channels for r in rows]
+
+
+def spread_plan(height, width, block_rows, n_shards, rank, n_frames, channels=3):
+    """The "spread" exchange of a step of n_frames frames (strong scaling):
+    every frame row-tiled over all ranks, frame k assembled on rank k % N, so
+    rank 0's xGMI ingress is 1/N of the step's bytes instead of (N-1)/N and
+    every rank's links carry their share (xGMI is point-to-point).
+    Returns (order, input_splits, output_splits, mine):
+    * order: the frames in the order each rank renders them (grouped by
+      destination rank, so each destination's rows are contiguous in the
+      send buffer (n_frames, rows_rank, width, channels));
+    * input_splits / output_splits: all_to_all_single sizes (elements);
+    * mine: the frames this rank assembles, in receive order (the receive
+      buffer is, per source shard s, (len(mine), rows_s, width, channels) -
+      assemble_frames with frames=len(mine))."""
+    dest = [k % n_shards for k in range(n_frames)]
+    order = [k for d in range(n_shards) for k in range(n_frames) if dest[k] == d]
+    cnt = [dest.count(d) for d in range(n_shards)]
+    rows = [len(shard_row_ids(height, block_rows, n_shards, s)) for s in range(n_shards)]
+    ins = [cnt[d] * rows[rank] * width * channels for d in range(n_shards)]
+    outs = [cnt[rank] * rows[s] * width * channels for s in range(n_shards)]
+    mine = [k for k in order if dest[k] == rank]
+    return order, ins, outs, mine
 
 
 def assembly_rows(height, block_rows, n_shards, frames):

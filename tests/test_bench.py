@@ -30,13 +30,35 @@ def run_bench(n, *args, timeout=240):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,frames", [(2, 3), (3, 5)])
+def test_config2_row_tiled_spread_default(n, frames):
+    """The default config2 shape at N>1: every frame of the step row-tiled
+    over the ranks (GL_RGBA8 shards packed to RGB8), one all-to-all assembling
+    frame k on rank k % N; every assembled frame equals its rank's own
+    whole-frame render byte for byte (bench.py checks, `verified`, summed over
+    the ranks), through the HIP kernel."""
+    line = run_bench(n, "--steps", "3", "--warmup", "1", "--frames", str(frames))
+    assert line["n_gpus"] == n and line["scaling"] == "strong" and line["value"] > 0
+    assert line["config"]["frames_per_step"] == frames and "all_to_all" in line["timing"]["collective"]
+    assert "GL_RGBA8" in line["config"]["output"] and "RGB8" in line["config"]["output"]
+    ranks = line["timing"]["per_rank"]
+    assert [r["rank"] for r in ranks] == list(range(n))
+    assert all(r["kernel_ms"] > 0 and r["collective_ms"] > 0 for r in ranks)
+    rows0 = 8 * len(range(0, 135, n))  # rank 0's 8-row blocks of the 135
+    assert line["roofline"]["bytes_per_launch"] == frames * 1920 * rows0 * 4
+    assert line["roofline"]["frac_float4_equivalent"] == pytest.approx(4 * line["roofline"]["frac"], rel=1e-3)
+    v = line["verified"]
+    assert v["bit_exact"] and v["frames_checked"] == frames and v["mismatched_pixels"] == 0
+    ind = line["independent_frames"]
+    assert ind["frames_per_step"] == n * frames and ind["scaling"] == "weak" and ind["value"] > 0
+
+
+@pytest.mark.gpu
 def test_config2_two_ranks_row_tiled_gather():
-    """The default config2 shape at N>1 (north_star): every frame row-tiled
-    over the ranks, the GL_RGBA8 shards gathered to rank 0 and
-    de-interleaved there; the assembled frames equal rank 0's whole-frame
-    render byte for byte (bench.py checks, `verified`), through the HIP
-    kernel."""
-    line = run_bench(2, "--steps", "3", "--warmup", "1", "--frames", "3")
+    """--frame-exchange gather (north_star's literal shape): the GL_RGBA8
+    shards of every frame gathered to rank 0 and de-interleaved there; the
+    assembled frames equal rank 0's whole-frame render byte for byte."""
+    line = run_bench(2, "--steps", "3", "--warmup", "1", "--frames", "3", "--frame-exchange", "gather")
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
     assert line["config"]["frames_per_step"] == 3 and "gather" in line["timing"]["collective"]
     assert "GL_RGBA8" in line["config"]["output"] and "RGB8" in line["config"]["output"]

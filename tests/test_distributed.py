@@ -238,3 +238,58 @@ def test_rgb8_shards_gather_contiguously_to_rank0(tmp_path, world):
     full = np.stack([rt.pack_rgba8(oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, t)) for t in TIMES])
     assert np.all(full[..., 3] == 0)
     assert np.array_equal(np.load(out), full[..., :3])
+
+
+def spread_worker(rank, world, port, result_path, n_frames):
+    """bench.py config2 at N ranks, the default --frame-exchange spread: the
+    step's F frames row-tiled over all ranks (rendered in spread_plan's
+    order, grouped by destination), packed to RGB8, one all-to-all delivers
+    frame k's shards to rank k % N, which de-interleaves them
+    (frame.spread_plan / assemble_frames)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import openglraytracer_amd as rt
+    from openglraytracer_amd import frame
+    from oracle import port as oracle_port, scenes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    objs = scenes.bench_objects(16)
+    ids = frame.shard_row_ids(H, BLOCK, world, rank)
+    order, ins, outs, mine = frame.spread_plan(H, W, BLOCK, world, rank, n_frames, channels=3)
+    # rt_render_batch of the views in `order`, shard `rank`, RT_OUTPUT_RGBA8
+    data = np.stack([rt.pack_rgba8(np.concatenate([oracle_port.render(objs, W, H, DEPTH, k / 60.0,
+                                                                      rows=(int(r), int(r) + 1)) for r in ids]))
+                     for k in order])
+    texels = torch.from_numpy(np.ascontiguousarray(data).view(np.int32).reshape(-1))
+    send = frame.pack_rgb8(texels, torch.empty(texels.numel() * 3, dtype=torch.uint8))
+    assert send.numel() == sum(ins)
+    recv = torch.empty(sum(outs), dtype=torch.uint8)
+    dist.all_to_all_single(recv, send, outs, ins)  # frame k -> rank k % N
+    got = frame.assemble_frames(recv, len(mine), H, W, BLOCK, world, channels=3).numpy() if mine else None
+    np.save(result_path + ".%d.npy" % rank, np.array(mine))
+    if mine:
+        np.save(result_path + ".%d.frames.npy" % rank, got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_frames", [(2, 5), (3, 5), (4, 3)])
+def test_spread_exchange_assembles_every_frame_once(tmp_path, world, n_frames):
+    """Every frame of the step lands whole on exactly one rank (k % N), byte
+    for byte the GL_RGBA8 texels of the whole-frame render without alpha;
+    uneven counts (5 frames on 2 or 3 ranks) and idle ranks (3 frames on 4)."""
+    import openglraytracer_amd as rt
+    from oracle import port as oracle_port, scenes
+    out = str(tmp_path / "spread")
+    mp.start_processes(spread_worker, args=(world, free_port(), out, n_frames), nprocs=world, start_method="spawn")
+    seen = []
+    for r in range(world):
+        mine = list(np.load(out + ".%d.npy" % r))
+        assert all(k % world == r for k in mine)
+        seen += mine
+        if mine:
+            got = np.load(out + ".%d.frames.npy" % r)
+            for j, k in enumerate(mine):
+                full = rt.pack_rgba8(oracle_port.render(scenes.bench_objects(16), W, H, DEPTH, k / 60.0))
+                assert np.array_equal(got[j], full[..., :3]), (r, k)
+    assert sorted(seen) == list(range(n_frames))

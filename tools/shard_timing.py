@@ -93,10 +93,44 @@ def main():
                             rt.render_shard(ctx, scene, buf.data_ptr(), W, H, depth, BLOCK, n, s, view=view,
                                             stream=sh)
                 per_shard.append(timed(fn, reps, stream))
+            if wl == "config2":
+                # the same launches alternating between two streams and two
+                # output buffers (consecutive steps' launches free to overlap:
+                # step i+1's ramp under step i's tail)
+                s2 = torch.cuda.Stream()
+                buf2 = torch.empty_like(buf)
+                flip = [0]
+
+                def alt():
+                    k = flip[0]
+                    flip[0] ^= 1
+                    st, bb = (stream, buf) if k == 0 else (s2, buf2)
+                    rt.render_batch(ctx, scene, bb.data_ptr(), W, H, depth, views, BLOCK, n, 0,
+                                    stream=st.cuda_stream)
+
+                def timed2(reps, rounds=5):
+                    out = []
+                    for _ in range(rounds):
+                        for _ in range(reps // 2):
+                            alt()
+                        torch.cuda.synchronize()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record(stream)
+                        s2.wait_stream(stream)
+                        for _ in range(reps):
+                            alt()
+                        stream.wait_stream(s2)
+                        e1.record(stream)
+                        torch.cuda.synchronize()
+                        out.append(e0.elapsed_time(e1) / reps)
+                    return float(np.median(out))
+                two_streams = timed2(reps)
             rec = {"workload": wl, "n": n, "frames_per_step": F, "kernel_ms_per_shard": [round(v, 5) for v in
                                                                                           per_shard],
                    "kernel_ms_max": round(max(per_shard), 5), "kernel_ms_mean": round(float(np.mean(per_shard)), 5)}
             px_shard = F * rows_max * W
+            if wl == "config2":
+                rec["shard0_two_streams_ms"] = round(two_streams, 5)
             rec["send_bytes_per_rank"] = px_shard * bpp_send
             rec["rank0_ingress_bytes"] = (n - 1) * px_shard * bpp_send
             if n > 1:
