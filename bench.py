@@ -264,6 +264,15 @@ def main():
     # stream `comm_s` orders the collectives (RCCL runs on its own stream
     # behind it) and the frame assembly.
     render_s = torch.cuda.Stream()
+    # N>1 steps render on two streams in turn (step i on render_streams[i % 2],
+    # into buffer slot i % 2): step i+1's launch may start while step i's
+    # drains (its last waves), as consecutive frames of a pipelined frame
+    # loop; the slot's previous exchange must have read the buffer first (the
+    # `freed` events). Measured on one MI355X (tools/shard_timing.py,
+    # profiles/r04c_shard_timing.log): rank 0's config-2 step at N = 8
+    # 56.2 -> 46.0 us, N = 2 185.5 -> 174.9 us.
+    render_streams = [render_s, torch.cuda.Stream()]
+    cur = {"s": render_s}
     comm_s = torch.cuda.Stream()
     torch.cuda.set_stream(comm_s)
     sh = render_s.cuda_stream
@@ -314,7 +323,7 @@ def main():
         def render(buf):
             for j, vs in chunks:
                 rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * frame_elems, W, H, DEPTH, vs,
-                                BLOCK_ROWS, world, rank, stream=sh)
+                                BLOCK_ROWS, world, rank, stream=cur["s"].cuda_stream)
         if mode == "gather" and surf == "rgba8":
             # GL_RGBA8 shards sent without their alpha byte (always 0, :404):
             # 3 B per pixel through rank 0's xGMI ingress instead of 4; the
@@ -380,7 +389,7 @@ def main():
         def render(buf):
             for j, vs in chunks:
                 rt.render_batch(ctx, scene, buf.data_ptr() + 4 * j * frame_elems, W, H, DEPTH, vs,
-                                BLOCK_ROWS, world, rank, stream=sh)
+                                BLOCK_ROWS, world, rank, stream=cur["s"].cuda_stream)
 
         def collective(slot, src):
             frame.pack_rgb8(src, sends[slot])
@@ -420,7 +429,7 @@ def main():
                 return frame.assemble_contiguous(bigs[slot], 1, H, W, ch, idx)
             return None
         return Plan(bufs, lambda buf: rt.render_shard(ctx, scene, buf.data_ptr(), W, H, DEPTH, BLOCK_ROWS, world,
-                                                      rank, view=view, stream=sh),
+                                                      rank, view=view, stream=cur["s"].cuda_stream),
                     W * H, W * rows_mine, 4 * ch, 1, collective, assemble)
 
     def measure(plan, steps, warmup):
@@ -438,16 +447,18 @@ def main():
                 plan.render(plan.bufs[0])
                 return
             slot = it % len(plan.bufs)
+            rs = render_streams[slot] if plan.collective is not None else render_s
+            cur["s"] = rs
             if freed[slot] is not None:
-                render_s.wait_event(freed[slot])  # the collective of step it-2 has read bufs[slot]
+                rs.wait_event(freed[slot])  # the collective of step it-2 has read bufs[slot]
             if timed:
-                kt.start(it, render_s)
+                kt.start(it, rs)
             plan.render(plan.bufs[slot])
             if timed:
-                kt.stop(it, render_s)
+                kt.stop(it, rs)
             if plan.collective is None:
                 return
-            rendered[slot].record(render_s)
+            rendered[slot].record(rs)
             comm_s.wait_event(rendered[slot])
             src = plan.bufs[slot] if coll_dev == "cuda" else plan.bufs[slot].cpu()
             if timed:
