@@ -103,7 +103,8 @@ constexpr int kGMaskMaxSpheres = 256;
 constexpr int kGMaskTexels = RT_GMASK_TEXELS;
 // The same wide masks as short candidate lists, one 16-B record per (live
 // light, texel): byte 0 = the number of candidate spheres (0..15), bytes
-// 1..15 = their slots (< 256), ascending; kGListOverflow in byte 0: more than
+// 1..15 = their slots (< 256), the sphere of the largest angular size from
+// the light first (rt_scene.cpp); kGListOverflow in byte 0: more than
 // 15 candidates, use the texel's mask words. A query then walks its own list:
 // a wave loops max-over-lanes-of-count times, once per candidate, instead of
 // once per set bit per mask word (the sum over the words of the per-word

@@ -1013,8 +1013,36 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         // the candidate lists of the same texels (rt_internal.h kGListMax)
         const size_t n_texels = gmask.size() / static_cast<size_t>(ds.gmask_words);
         glist.assign(n_texels * 16, 0);
+        // each live light's order of the spheres: largest angular size seen
+        // from the light first (a light inside a sphere's inflated bound, or
+        // a non-finite sphere, first of all), so a shadowed query meets its
+        // occluder early and its any-hit walk ends (the result is
+        // order-independent). CPU model (tools/model/shadow_model.py): the
+        // wave's candidate passes per shadow call 2.34 -> 1.47 on config 4,
+        // 0.95 -> 0.73 on config 3.
+        std::vector<int> live;
+        for (int j = 0; j < n_lights; ++j)
+            if (lrec[j].dead == 0.0f) live.push_back(j);
+        std::vector<std::vector<int>> rank_of(live.size(), std::vector<int>(sph.size()));
+        for (size_t k = 0; k < live.size(); ++k) {
+            const rt_light &L = lights[live[k]];
+            std::vector<double> key(sph.size());
+            for (size_t q = 0; q < sph.size(); ++q) {
+                const double v[3] = {double(sph[q].cx) - L.position[0], double(sph[q].cy) - L.position[1],
+                                     double(sph[q].cz) - L.position[2]};
+                const double d = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+                const double r = double(smeta[q].radius);
+                key[q] = (std::isfinite(d) && std::isfinite(r) && d > r + 0.021 + 1e-3 * d) ? r / d : HUGE_VAL;
+            }
+            std::vector<int> order(sph.size());
+            for (size_t q = 0; q < sph.size(); ++q) order[q] = static_cast<int>(q);
+            std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] > key[y]; });
+            for (size_t q = 0; q < order.size(); ++q) rank_of[k][order[q]] = static_cast<int>(q);
+        }
+        const size_t per_light = n_texels / (live.empty() ? 1 : live.size());
         for (size_t t = 0; t < n_texels; ++t) {
             uint8_t *rec = glist.data() + t * 16;
+            const std::vector<int> &rk = rank_of[t / per_light];
             int n = 0;
             // the same truncation as the kernel's word walk (occluded: the
             // last word masked to the `rest` = ns - 64 w live slots)
@@ -1029,6 +1057,8 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
                 }
             }
             rec[0] = n <= kGListMax ? static_cast<uint8_t>(n) : static_cast<uint8_t>(kGListOverflow);
+            if (n <= kGListMax)
+                std::sort(rec + 1, rec + 1 + n, [&](uint8_t x, uint8_t y) { return rk[x] < rk[y]; });
         }
         ds.off_glist = off;
         off += units(glist.size());

@@ -1,0 +1,161 @@
+"""CPU model of the wide-mask shadow queries' candidate passes per wave (development probe).
+
+    python tools/model/shadow_model.py [--config config4] [--tiles 64] [--seed 1]
+
+Scenes of 33-256 spheres answer a shadow query (rt_kernel.hip occluded_impl,
+raytrace_compute.glsl:807-819) by walking the candidate list of the lane's
+direction texel from the light (one 16-B record per live light and texel:
+count + up to 15 sphere slots, rt_scene.cpp); the walk is any-hit, so a lane
+leaves at its first occluder, and the wave loops as many passes as its
+slowest lane needs. The lists hold the slots in ascending order. Ordering a
+texel's candidates by the sphere's angular size from the light, largest
+first, lets a shadowed lane meet its occluder earlier (the result cannot
+change: any-hit is order-independent).
+
+The model takes the product's own lists (rt_debug_scene_blob), the config's
+rays from walk_model.py grouped per wave and walk iteration as trace_tree
+runs them, casts every hit's shadow ray to each live light (when the light
+is above the surface), finds each candidate's exact float64 segment hit and
+counts the wave's passes for both orders.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import bvh_model as bm  # noqa: E402
+import walk_model as wm  # noqa: E402
+
+rt = wm.rt
+NT = 64  # kGMaskTexels
+
+
+def scene_lists(n_spheres):
+    import ctypes as C
+    L = rt.lib()
+    f = L.rt_debug_scene_blob
+    f.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_longlong,
+                  C.c_void_p]
+    objs, mats, lights = rt.bench_objects(n_spheres, 0), rt.reference_materials(), rt.reference_lights()
+    oa = (rt.Object * len(objs))(*objs)
+    ma = (rt.Material * len(mats))(*mats)
+    la = (rt.Light * len(lights))(*lights)
+    meta = np.zeros(24, np.int32)
+    n = f(oa, len(objs), ma, len(mats), la, len(lights), None, 0, meta.ctypes.data)
+    buf = np.zeros(n, np.uint8)
+    f(oa, len(objs), ma, len(mats), la, len(lights), buf.ctypes.data, n, meta.ctypes.data)
+    off_sph, off_glist, ns = meta[1], meta[16], meta[17]
+    sph = buf.view(np.float32).reshape(-1, 4)[off_sph:off_sph + ns].astype(np.float64)
+    live = [j for j, lt in enumerate(lights) if any(lt.diffuse[k] or lt.specular[k] for k in range(4))]
+    per = 6 * NT * NT
+    glist = buf[off_glist * 16:off_glist * 16 + len(live) * per * 16].reshape(len(live), per, 16)
+    lpos = [np.array(lights[j].position[:], np.float64) for j in live]
+    return sph, glist, lpos
+
+
+def texel(u):
+    ax, ay, az = np.abs(u)
+    fx = ax >= ay and ax >= az
+    fy = (not fx) and ay >= az
+    um = u[0] if fx else (u[1] if fy else u[2])
+    ua = u[1] if fx else u[0]
+    ub = u[2] if (fy or fx) else u[1]
+    face = 2 * (0 if fx else (1 if fy else 2)) + (1 if um < 0 else 0)
+    am = abs(um)
+    if not (1e-20 < am < 1e30):
+        return -1
+    hh = 0.5 * NT / am
+    col = min(max(int(np.floor(ua * hh + 0.5 * NT)), 0), NT - 1)
+    row = min(max(int(np.floor(ub * hh + 0.5 * NT)), 0), NT - 1)
+    return (face * NT + row) * NT + col
+
+
+def blocks(sph, s, start, d):
+    c, rr = sph[s, :3], sph[s, 3]
+    oc = start - c
+    a = d @ d
+    b = 2 * (d @ oc)
+    cc = oc @ oc - rr
+    disc = b * b - 4 * a * cc
+    if disc < 0:
+        return False
+    sq = np.sqrt(disc)
+    t1, t2 = (-b - sq) / (2 * a), (-b + sq) / (2 * a)
+    t = t1 if t1 > 0 else t2
+    return 0 < t < 1
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="config4")
+    ap.add_argument("--tiles", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args()
+    w, h, nsph, depth = wm.CONFIGS[a.config]
+    S = wm.scene_arrays(nsph)
+    sph, glist, lpos = scene_lists(nsph)
+    rng = np.random.default_rng(a.seed)
+    wm.links.clear()
+    n_pix, pix, lev, hitl, cr, ct = wm.build_trees(S, w, h, depth, a.tiles, rng)
+    ro, rd = wm.build_trees.rays
+    hit, p, nrm, inside, mat = wm.trace(S, ro, rd)
+    tot = {"calls": 0, "queries": 0, "shadowed": 0, "passes_ascending": 0, "passes_by_size": 0, "tests_ascending": 0,
+           "tests_by_size": 0, "overflow": 0}
+    for t in range(a.tiles):
+        orders = []
+        for r in range(t * 64, (t + 1) * 64):
+            od = []
+            wm.lane_events(r, cr, ct, od)
+            orders.append(od)
+        for k in range(max(len(x) for x in orders)):
+            nodes = [x[k] if k < len(x) and hitl[x[k]] else -1 for x in orders]
+            for j, L in enumerate(lpos):
+                lanes_a, lanes_b = [], []
+                for nd in nodes:
+                    if nd < 0:
+                        continue
+                    sdir = L - p[nd]
+                    if sdir @ nrm[nd] <= 0:
+                        continue
+                    start = p[nd] + 0.01 * nrm[nd]
+                    tx = texel(-sdir)
+                    rec = glist[j, tx]
+                    cnt = int(rec[0])
+                    if cnt == 255:
+                        tot["overflow"] += 1
+                        continue
+                    cand = [int(s) for s in rec[1:1 + cnt]]
+                    size = [-(np.sqrt(sph[s, 3]) / max(np.linalg.norm(sph[s, :3] - L), 1e-9)) for s in cand]
+                    by_size = [cand[i] for i in np.argsort(size, kind="stable")]
+                    occ = {s for s in cand if blocks(sph, s, start, sdir)}
+                    tot["queries"] += 1
+                    tot["shadowed"] += bool(occ)
+
+                    def passes(lst):
+                        for i, s in enumerate(lst):
+                            if s in occ:
+                                return i + 1
+                        return len(lst)
+                    lanes_a.append(passes(cand))
+                    lanes_b.append(passes(by_size))
+                if lanes_a:
+                    tot["calls"] += 1
+                    tot["passes_ascending"] += max(lanes_a)
+                    tot["passes_by_size"] += max(lanes_b)
+                    tot["tests_ascending"] += sum(lanes_a)
+                    tot["tests_by_size"] += sum(lanes_b)
+    c, q = tot["calls"], tot["queries"]
+    print(json.dumps({"config": a.config, "tiles": a.tiles, "wave_calls": c, "queries": q,
+                      "shadowed_frac": round(tot["shadowed"] / q, 3), "overflow_queries": tot["overflow"],
+                      "passes_per_call": {"ascending": round(tot["passes_ascending"] / c, 3),
+                                          "by_angular_size": round(tot["passes_by_size"] / c, 3)},
+                      "exact_tests_per_query": {"ascending": round(tot["tests_ascending"] / q, 3),
+                                                "by_angular_size": round(tot["tests_by_size"] / q, 3)}}))
+
+
+if __name__ == "__main__":
+    main()
