@@ -7,16 +7,24 @@ raytrace_compute.glsl:807-819) by walking the candidate list of the lane's
 direction texel from the light (one 16-B record per live light and texel:
 count + up to 15 sphere slots, rt_scene.cpp); the walk is any-hit, so a lane
 leaves at its first occluder, and the wave loops as many passes as its
-slowest lane needs. The lists hold the slots in ascending order. Ordering a
-texel's candidates by the sphere's angular size from the light, largest
-first, lets a shadowed lane meet its occluder earlier (the result cannot
-change: any-hit is order-independent).
+slowest lane needs. Ordering a texel's candidates by the sphere's angular
+size from the light, largest first, lets a shadowed lane meet its occluder
+earlier (the result cannot change: any-hit is order-independent).
+
+Results (round 4): with the lists in ascending slot order, 2.34 passes per
+wave call on config 4 (RT_STATS measured 2.5) and 0.95 on config 3; by
+angular size 1.47 and 0.73 — built (rt_scene.cpp), measured config 4
+14.73 -> 14.00 ms, config 3 0.874 -> 0.861 ms, frames unchanged
+(profiles/r04d_ab_candidate_order.log). A texel-specific order (the cone
+covering the texel's centre most deeply first) reaches 1.36 / 0.70: about a
+further 0.7 % by the same ratio, below the 3 % bar; not built. "as_stored"
+below is whatever order the product's lists now hold.
 
 The model takes the product's own lists (rt_debug_scene_blob), the config's
 rays from walk_model.py grouped per wave and walk iteration as trace_tree
 runs them, casts every hit's shadow ray to each live light (when the light
 is above the surface), finds each candidate's exact float64 segment hit and
-counts the wave's passes for both orders.
+counts the wave's passes for each order.
 """
 import argparse
 import json
@@ -74,6 +82,19 @@ def texel(u):
     return (face * NT + row) * NT + col
 
 
+def texel_dir(t):
+    """Unit direction of texel t's centre (the inverse of texel())."""
+    face, rem = divmod(t, NT * NT)
+    row, col = divmod(rem, NT)
+    axis, neg = divmod(face, 2)
+    um = -1.0 if neg else 1.0
+    ua = (col + 0.5 - 0.5 * NT) / (0.5 * NT)
+    ub = (row + 0.5 - 0.5 * NT) / (0.5 * NT)
+    v = [(um, ua, ub), (ua, um, ub), (ua, ub, um)][axis]
+    v = np.array(v)
+    return v / np.linalg.norm(v)
+
+
 def blocks(sph, s, start, d):
     c, rr = sph[s, :3], sph[s, 3]
     oc = start - c
@@ -104,7 +125,7 @@ def main():
     ro, rd = wm.build_trees.rays
     hit, p, nrm, inside, mat = wm.trace(S, ro, rd)
     tot = {"calls": 0, "queries": 0, "shadowed": 0, "passes_ascending": 0, "passes_by_size": 0, "tests_ascending": 0,
-           "tests_by_size": 0, "overflow": 0}
+           "tests_by_size": 0, "overflow": 0, "passes_by_depth": 0, "tests_by_depth": 0}
     for t in range(a.tiles):
         orders = []
         for r in range(t * 64, (t + 1) * 64):
@@ -114,7 +135,7 @@ def main():
         for k in range(max(len(x) for x in orders)):
             nodes = [x[k] if k < len(x) and hitl[x[k]] else -1 for x in orders]
             for j, L in enumerate(lpos):
-                lanes_a, lanes_b = [], []
+                lanes_a, lanes_b, lanes_c = [], [], []
                 for nd in nodes:
                     if nd < 0:
                         continue
@@ -131,6 +152,16 @@ def main():
                     cand = [int(s) for s in rec[1:1 + cnt]]
                     size = [-(np.sqrt(sph[s, 3]) / max(np.linalg.norm(sph[s, :3] - L), 1e-9)) for s in cand]
                     by_size = [cand[i] for i in np.argsort(size, kind="stable")]
+                    # the texel-specific order: the sphere whose cone (from
+                    # the light) covers the texel's centre most deeply first
+                    tdir = texel_dir(tx)
+                    depth_key = []
+                    for s_ in cand:
+                        v = sph[s_, :3] - L
+                        dd = np.linalg.norm(v)
+                        half = np.arcsin(min(1.0, (np.sqrt(sph[s_, 3]) + 0.021 + 1e-3 * dd) / dd))
+                        depth_key.append(-(half - np.arccos(np.clip(v @ tdir / dd, -1, 1))))
+                    by_depth = [cand[i] for i in np.argsort(depth_key, kind="stable")]
                     occ = {s for s in cand if blocks(sph, s, start, sdir)}
                     tot["queries"] += 1
                     tot["shadowed"] += bool(occ)
@@ -142,19 +173,24 @@ def main():
                         return len(lst)
                     lanes_a.append(passes(cand))
                     lanes_b.append(passes(by_size))
+                    lanes_c.append(passes(by_depth))
                 if lanes_a:
                     tot["calls"] += 1
                     tot["passes_ascending"] += max(lanes_a)
                     tot["passes_by_size"] += max(lanes_b)
                     tot["tests_ascending"] += sum(lanes_a)
                     tot["tests_by_size"] += sum(lanes_b)
+                    tot["passes_by_depth"] += max(lanes_c)
+                    tot["tests_by_depth"] += sum(lanes_c)
     c, q = tot["calls"], tot["queries"]
     print(json.dumps({"config": a.config, "tiles": a.tiles, "wave_calls": c, "queries": q,
                       "shadowed_frac": round(tot["shadowed"] / q, 3), "overflow_queries": tot["overflow"],
-                      "passes_per_call": {"ascending": round(tot["passes_ascending"] / c, 3),
-                                          "by_angular_size": round(tot["passes_by_size"] / c, 3)},
-                      "exact_tests_per_query": {"ascending": round(tot["tests_ascending"] / q, 3),
-                                                "by_angular_size": round(tot["tests_by_size"] / q, 3)}}))
+                      "passes_per_call": {"as_stored": round(tot["passes_ascending"] / c, 3),
+                                          "by_angular_size": round(tot["passes_by_size"] / c, 3),
+                                          "by_texel_depth": round(tot["passes_by_depth"] / c, 3)},
+                      "exact_tests_per_query": {"as_stored": round(tot["tests_ascending"] / q, 3),
+                                                "by_angular_size": round(tot["tests_by_size"] / q, 3),
+                                                "by_texel_depth": round(tot["tests_by_depth"] / q, 3)}}))
 
 
 if __name__ == "__main__":
