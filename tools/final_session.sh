@@ -1,25 +1,41 @@
 #!/bin/bash
-# Same-build profile + bench session (run through gpurun): PMC passes of every
-# bench workload, their summaries written to profiles/ on the box (so the bench
-# lines that follow take traffic / valu from the same sources), then the bench
-# lines; everything copied under gpurun_out/TAG to travel back.
-# usage: tools/final_session.sh TAG
+# Same-build profile + bench session (run through gpurun), in two calls that
+# each fit one gpurun limit:
+#   tools/final_session.sh TAG prof    PMC passes of every bench workload; their
+#                                      summaries go to profiles/ on the box and
+#                                      travel back under gpurun_out/TAG/profiles
+#                                      (copy them into profiles/ before the bench
+#                                      call, so its lines take traffic / valu from
+#                                      the same sources)
+#   tools/final_session.sh TAG bench   the bench lines of every workload, smoke,
+#                                      and a gloo rehearsal of config 2 at N = 4
+#   tools/final_session.sh TAG         both, in one call
 set -uo pipefail
 tag=${1:?tag}
+what=${2:-all}
 out=gpurun_out/$tag; mkdir -p $out
 export TMPDIR=/tmp
 run() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 $t "$@" > $out/$name.log 2>&1; local rc=$?; echo "   rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-run prof_config4 900 tools/profile.sh $tag/c4 --workload config4 --steps 3 --warmup 1
-run prof_config3 900 tools/profile.sh $tag/c3 --workload config3 --steps 10 --warmup 2
-run prof_config2 900 tools/profile.sh $tag/c2 --steps 50 --warmup 5
-run prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
-run sum2 60 python tools/pmc_summary.py $out/c2 profiles/${tag}_config2 8 config2
-run sum3 60 python tools/pmc_summary.py $out/c3 profiles/${tag}_config3 1 config3
-run sum4 60 python tools/pmc_summary.py $out/c4 profiles/${tag}_config4 1 config4
-run sum5 60 python tools/pmc_summary.py $out/c5 profiles/${tag}_config5 1 config5
-run bench_config2 300 python bench.py
-run bench_config3 300 python bench.py --workload config3 --steps 20 --warmup 3 --no-cpu-baseline
-run bench_config4 300 python bench.py --workload config4 --steps 5 --warmup 1 --no-cpu-baseline
-run bench_config5 300 python bench.py --workload config5 --steps 3 --warmup 1 --no-cpu-baseline
-mkdir -p $out/profiles && cp profiles/${tag}_* profiles/pmc_*latest.json $out/profiles/
+if [ "$what" = prof ] || [ "$what" = all ]; then
+  run prof_config4 900 tools/profile.sh $tag/c4 --workload config4 --steps 3 --warmup 1
+  run prof_config3 900 tools/profile.sh $tag/c3 --workload config3 --steps 10 --warmup 2
+  run prof_config2 900 tools/profile.sh $tag/c2 --steps 50 --warmup 5
+  run prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
+  run sum2 60 python tools/pmc_summary.py $out/c2 profiles/${tag}_config2 8 config2
+  run sum3 60 python tools/pmc_summary.py $out/c3 profiles/${tag}_config3 1 config3
+  run sum4 60 python tools/pmc_summary.py $out/c4 profiles/${tag}_config4 1 config4
+  run sum5 60 python tools/pmc_summary.py $out/c5 profiles/${tag}_config5 1 config5
+  mkdir -p $out/profiles && cp profiles/${tag}_* profiles/pmc_*latest.json $out/profiles/
+fi
+if [ "$what" = bench ] || [ "$what" = all ]; then
+  run bench_config2 300 python bench.py
+  run bench_config3 300 python bench.py --workload config3 --steps 20 --warmup 3 --no-cpu-baseline
+  run bench_config4 300 python bench.py --workload config4 --steps 5 --warmup 1 --no-cpu-baseline
+  run bench_config5 300 python bench.py --workload config5 --steps 3 --warmup 1 --no-cpu-baseline
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  # several ranks share the one GPU here (gloo): the step structure and the
+  # byte-exact assembly, not scaling figures
+  run gloo_config2_n4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+      --master-port 29611 bench.py --gpus 4 --dist-backend gloo --steps 5 --warmup 2 --no-cpu-baseline
+fi
 echo done

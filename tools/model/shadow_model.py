@@ -56,16 +56,30 @@ def scene_lists(n_spheres):
     n = f(oa, len(objs), ma, len(mats), la, len(lights), None, 0, meta.ctypes.data)
     buf = np.zeros(n, np.uint8)
     f(oa, len(objs), ma, len(mats), la, len(lights), buf.ctypes.data, n, meta.ctypes.data)
-    off_sph, off_glist, ns = meta[1], meta[16], meta[17]
+    off_sph, off_dmask, dmask_n, dmask_bytes, off_glist, ns = meta[1], meta[11], meta[12], meta[13], meta[16], meta[17]
     sph = buf.view(np.float32).reshape(-1, 4)[off_sph:off_sph + ns].astype(np.float64)
     live = [j for j, lt in enumerate(lights) if any(lt.diffuse[k] or lt.specular[k] for k in range(4))]
+    lpos = [np.array(lights[j].position[:], np.float64) for j in live]
+    if off_glist < 0:
+        # LDS direction masks (<= 64 spheres, the depth-0/1 path): one mask
+        # word per (live light, texel), dmask_n texels per face edge; the
+        # kernel walks the set bits in ascending slot order. As lists:
+        per = 6 * dmask_n * dmask_n
+        raw = buf[off_dmask * 16:off_dmask * 16 + len(live) * per * dmask_bytes]
+        words = raw.view({2: np.uint16, 4: np.uint32, 8: np.uint64}[int(dmask_bytes)]).reshape(len(live), per)
+        glist = np.zeros((len(live), per, 65), np.int32)
+        for j in range(len(live)):
+            for t in range(per):
+                bits = [q for q in range(ns) if (int(words[j, t]) >> q) & 1]
+                glist[j, t, 0] = len(bits)
+                glist[j, t, 1:1 + len(bits)] = bits
+        return sph, glist, lpos, int(dmask_n)
     per = 6 * NT * NT
     glist = buf[off_glist * 16:off_glist * 16 + len(live) * per * 16].reshape(len(live), per, 16)
-    lpos = [np.array(lights[j].position[:], np.float64) for j in live]
-    return sph, glist, lpos
+    return sph, glist, lpos, NT
 
 
-def texel(u):
+def texel(u, NT=NT):
     ax, ay, az = np.abs(u)
     fx = ax >= ay and ax >= az
     fy = (not fx) and ay >= az
@@ -82,7 +96,7 @@ def texel(u):
     return (face * NT + row) * NT + col
 
 
-def texel_dir(t):
+def texel_dir(t, NT=NT):
     """Unit direction of texel t's centre (the inverse of texel())."""
     face, rem = divmod(t, NT * NT)
     row, col = divmod(rem, NT)
@@ -118,7 +132,7 @@ def main():
     a = ap.parse_args()
     w, h, nsph, depth = wm.CONFIGS[a.config]
     S = wm.scene_arrays(nsph)
-    sph, glist, lpos = scene_lists(nsph)
+    sph, glist, lpos, nt = scene_lists(nsph)
     rng = np.random.default_rng(a.seed)
     wm.links.clear()
     n_pix, pix, lev, hitl, cr, ct = wm.build_trees(S, w, h, depth, a.tiles, rng)
@@ -143,10 +157,10 @@ def main():
                     if sdir @ nrm[nd] <= 0:
                         continue
                     start = p[nd] + 0.01 * nrm[nd]
-                    tx = texel(-sdir)
+                    tx = texel(-sdir, nt)
                     rec = glist[j, tx]
                     cnt = int(rec[0])
-                    if cnt == 255:
+                    if cnt == 255 and nt == NT:
                         tot["overflow"] += 1
                         continue
                     cand = [int(s) for s in rec[1:1 + cnt]]
@@ -154,7 +168,7 @@ def main():
                     by_size = [cand[i] for i in np.argsort(size, kind="stable")]
                     # the texel-specific order: the sphere whose cone (from
                     # the light) covers the texel's centre most deeply first
-                    tdir = texel_dir(tx)
+                    tdir = texel_dir(tx, nt)
                     depth_key = []
                     for s_ in cand:
                         v = sph[s_, :3] - L

@@ -52,7 +52,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 import openglraytracer_amd as rt  # noqa: E402  (host-side scene / camera helpers only)
 
-CONFIGS = {"config3": (3840, 2160, 64, 2), "config4": (7680, 4320, 256, 4)}
+CONFIGS = {"config2": (1920, 1080, 16, 0), "config3": (3840, 2160, 64, 2), "config4": (7680, 4320, 256, 4)}
 
 
 def scene_arrays(n_spheres):
