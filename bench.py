@@ -563,7 +563,7 @@ def main():
             dist.all_reduce(t)
             bad, px = int(t[0].item()), int(t[1].item())
         return {"frames_checked": px // (H * W), "pixels": px, "mismatched_pixels": bad, "bit_exact": bad == 0,
-                "against": "rank 0's own whole-frame render of the same frames, same surface"}
+                "against": "the assembling rank's own whole-frame render of the same frames, same surface"}
 
     view = None
     if batched:
