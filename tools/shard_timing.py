@@ -93,7 +93,7 @@ def main():
                             rt.render_shard(ctx, scene, buf.data_ptr(), W, H, depth, BLOCK, n, s, view=view,
                                             stream=sh)
                 per_shard.append(timed(fn, reps, stream))
-            if wl == "config2":
+            if True:
                 # the same launches alternating between two streams and two
                 # output buffers (consecutive steps' launches free to overlap:
                 # step i+1's ramp under step i's tail)
@@ -105,8 +105,14 @@ def main():
                     k = flip[0]
                     flip[0] ^= 1
                     st, bb = (stream, buf) if k == 0 else (s2, buf2)
-                    rt.render_batch(ctx, scene, bb.data_ptr(), W, H, depth, views, BLOCK, n, 0,
-                                    stream=st.cuda_stream)
+                    if wl == "config2":
+                        rt.render_batch(ctx, scene, bb.data_ptr(), W, H, depth, views, BLOCK, n, 0,
+                                        stream=st.cuda_stream)
+                    elif n == 1:
+                        rt.render_device(ctx, scene, bb.data_ptr(), W, H, depth, view=view, stream=st.cuda_stream)
+                    else:
+                        rt.render_shard(ctx, scene, bb.data_ptr(), W, H, depth, BLOCK, n, 0, view=view,
+                                        stream=st.cuda_stream)
 
                 def timed2(reps, rounds=5):
                     out = []
@@ -129,8 +135,7 @@ def main():
                                                                                           per_shard],
                    "kernel_ms_max": round(max(per_shard), 5), "kernel_ms_mean": round(float(np.mean(per_shard)), 5)}
             px_shard = F * rows_max * W
-            if wl == "config2":
-                rec["shard0_two_streams_ms"] = round(two_streams, 5)
+            rec["shard0_two_streams_ms"] = round(two_streams, 5)
             rec["send_bytes_per_rank"] = px_shard * bpp_send
             rec["rank0_ingress_bytes"] = (n - 1) * px_shard * bpp_send
             if n > 1:
