@@ -48,12 +48,18 @@ the 1920x1080 frame at 1024 jittered samples per pixel, samples sharded over
 the N ranks, partial sums combined with one RCCL all-reduce: strong scaling;
 value = samples/s.
 
+Consecutive steps alternate between two render streams and two output
+buffers (--single-stream: one of each), so a launch's last waves overlap the
+next step's launch, as consecutive frames of a pipelined frame loop; every
+frame is still rendered in full, and each launch is timed on its own stream.
+
 value = primary rays (samples) of the step / step time (max over ranks), Mrays/s.
 roofline = the render kernel against the HBM-write roofline: bytes stored per
 launch (16 B per pixel for a float4 frame, 12 for float3 shards, 4 for RGBA8)
-/ average kernel time from HIP events on the launch stream (one pair around
-the back-to-back launches of the timed region when a step has no collective;
-otherwise a pair around every step's launches). Its `traffic` and `valu`
+/ average kernel time from HIP events on the launch stream (a pair around
+every step's launches on its stream: each launch's own duration, overlap
+included, as rocprofv3 reports it; with --single-stream and no collective,
+one pair around the back-to-back launches of the timed region). Its `traffic` and `valu`
 come from the committed rocprofv3 PMC summary of the same sources
 (profiles/pmc_<workload>_latest.json), else they say which build they belong to.
 cpu_baseline = the reference's own shader on Mesa llvmpipe (oracle/_ref) on the
@@ -117,6 +123,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0,
                     help="approximate budget of the llvmpipe baseline samples")
+    ap.add_argument("--single-stream", action="store_true",
+                    help="render every step on one stream (default: consecutive steps alternate between two "
+                         "streams and two buffers, so a launch's last waves overlap the next launch)")
     ap.add_argument("--no-rgba8", action="store_true",
                     help="config2 at N=1: skip the same-surface (GL_RGBA8) measurement")
     ap.add_argument("--no-single-frame", action="store_true",
@@ -297,16 +306,24 @@ def main():
         ch, dt, _ = surface(surf)
         esize = 4  # bytes per element (float32 / int32)
         if mode == "none" or world == 1:
-            # frames [rF, (r+1)F) whole on rank r, in place, launches back to back
+            # frames [rF, (r+1)F) whole on rank r, launches back to back, the
+            # steps alternating between two streams and two buffers (step
+            # i+1's launch under step i's last waves; --single-stream: one
+            # stream, one buffer)
             views = [rt.make_view(None, frame_time(rank * F + k)) for k in range(F)]
-            bufs = [torch.zeros(F * H * W * ch, dtype=dt, device="cuda")]
+            bufs = [torch.zeros(F * H * W * ch, dtype=dt, device="cuda")
+                    for _ in range(1 if args.single_stream else 2)]
             chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, F, rt.abi.RT_MAX_BATCH)]
 
             def render(buf):
                 for j, vs in chunks:
-                    rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * H * W * ch, W, H, DEPTH, vs, stream=sh)
+                    rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * H * W * ch, W, H, DEPTH, vs,
+                                    stream=cur["s"].cuda_stream)
+            # (two streams: an event pair around every step's launches on its
+            # stream, so kernel_ms is each launch's own duration, overlap
+            # included, as rocprofv3 reports it; the step time is shorter)
             return Plan(bufs, render, world * F * W * H, W * H * F // len(chunks), esize * ch, len(chunks),
-                        per_launch=False)
+                        per_launch=not args.single_stream)
         if mode == "spread":
             return spread_plan()
         n_frames = F if mode == "gather" else world * F
@@ -409,9 +426,11 @@ def main():
         ch, dt, _ = surface("rgba32f" if world == 1 else "rgb32f")
         view = rt.make_view(None, 0.0)
         if world == 1:
-            bufs = [torch.zeros(H * W * 4, dtype=dt, device="cuda")]
+            # consecutive steps on two streams and buffers (the next frame's
+            # launch under this one's last wave tiles) unless --single-stream
+            bufs = [torch.zeros(H * W * 4, dtype=dt, device="cuda") for _ in range(1 if args.single_stream else 2)]
             return Plan(bufs, lambda buf: rt.render_device(ctx, scene, buf.data_ptr(), W, H, DEPTH, view=view,
-                                                           stream=sh), W * H, W * H, 16)
+                                                           stream=cur["s"].cuda_stream), W * H, W * H, 16)
         rows_mine = rt.shard_rows(H, BLOCK_ROWS, world, rank)
         elems = frame.flat_shard_elems(1, H, W, BLOCK_ROWS, world, ch)
         bufs = [torch.zeros(elems, dtype=dt, device="cuda") for _ in range(2)]
@@ -443,11 +462,11 @@ def main():
         freed = [None] * len(plan.bufs)  # event: the collective has finished reading bufs[slot]
 
         def step(timed, it):
-            if not plan.per_launch:  # frames rendered in place, launches back to back
+            if not plan.per_launch:  # frames rendered in place, launches back to back (--single-stream)
                 plan.render(plan.bufs[0])
                 return
             slot = it % len(plan.bufs)
-            rs = render_streams[slot] if plan.collective is not None else render_s
+            rs = render_streams[slot]
             cur["s"] = rs
             if freed[slot] is not None:
                 rs.wait_event(freed[slot])  # the collective of step it-2 has read bufs[slot]
