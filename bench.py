@@ -48,18 +48,19 @@ the 1920x1080 frame at 1024 jittered samples per pixel, samples sharded over
 the N ranks, partial sums combined with one RCCL all-reduce: strong scaling;
 value = samples/s.
 
-Consecutive steps alternate between two render streams and two output
-buffers (--single-stream: one of each), so a launch's last waves overlap the
-next step's launch, as consecutive frames of a pipelined frame loop; every
-frame is still rendered in full, and each launch is timed on its own stream.
+At N>1 consecutive steps alternate between two render streams and two output
+buffers (--streams 2), so a launch's last waves overlap the next step's
+launch, as consecutive frames of a pipelined frame loop; every frame is still
+rendered in full. At N=1 the line's value and roofline are one stream's
+(each launch alone on the GPU); the two-stream rate is the `pipelined` field.
 
 value = primary rays (samples) of the step / step time (max over ranks), Mrays/s.
 roofline = the render kernel against the HBM-write roofline: bytes stored per
 launch (16 B per pixel for a float4 frame, 12 for float3 shards, 4 for RGBA8)
-/ average kernel time from HIP events on the launch stream (a pair around
-every step's launches on its stream: each launch's own duration, overlap
-included, as rocprofv3 reports it; with --single-stream and no collective,
-one pair around the back-to-back launches of the timed region). Its `traffic` and `valu`
+/ average kernel time from HIP events on the launch stream (one pair around
+the back-to-back launches of the timed region at N=1; at N>1 a pair around
+every step's launches on its stream, which includes any overlap with the
+neighbouring step's launch). Its `traffic` and `valu`
 come from the committed rocprofv3 PMC summary of the same sources
 (profiles/pmc_<workload>_latest.json), else they say which build they belong to.
 cpu_baseline = the reference's own shader on Mesa llvmpipe (oracle/_ref) on the
@@ -123,9 +124,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0,
                     help="approximate budget of the llvmpipe baseline samples")
-    ap.add_argument("--single-stream", action="store_true",
-                    help="render every step on one stream (default: consecutive steps alternate between two "
-                         "streams and two buffers, so a launch's last waves overlap the next launch)")
+    ap.add_argument("--streams", type=int, choices=[1, 2], default=None,
+                    help="render streams the steps alternate between (with as many output buffers): 2 lets a "
+                         "launch's last waves overlap the next step's launch; default 1 at N=1 (each launch alone "
+                         "on the GPU, so its HIP-event duration is the kernel's, as rocprofv3 reports it; the "
+                         "two-stream rate is the secondary `pipelined` field) and 2 at N>1")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="N=1: skip the secondary two-stream (`pipelined`) measurement")
     ap.add_argument("--no-rgba8", action="store_true",
                     help="config2 at N=1: skip the same-surface (GL_RGBA8) measurement")
     ap.add_argument("--no-single-frame", action="store_true",
@@ -282,6 +287,7 @@ def main():
     # 56.2 -> 46.0 us, N = 2 185.5 -> 174.9 us.
     render_streams = [render_s, torch.cuda.Stream()]
     cur = {"s": render_s}
+    n_streams = {"n": args.streams or (1 if world == 1 else 2)}  # read by the plan builders
     comm_s = torch.cuda.Stream()
     torch.cuda.set_stream(comm_s)
     sh = render_s.cuda_stream
@@ -306,13 +312,11 @@ def main():
         ch, dt, _ = surface(surf)
         esize = 4  # bytes per element (float32 / int32)
         if mode == "none" or world == 1:
-            # frames [rF, (r+1)F) whole on rank r, launches back to back, the
-            # steps alternating between two streams and two buffers (step
-            # i+1's launch under step i's last waves; --single-stream: one
-            # stream, one buffer)
+            # frames [rF, (r+1)F) whole on rank r, launches back to back (with
+            # two streams: the steps alternating between two streams and two
+            # buffers, step i+1's launch under step i's last waves)
             views = [rt.make_view(None, frame_time(rank * F + k)) for k in range(F)]
-            bufs = [torch.zeros(F * H * W * ch, dtype=dt, device="cuda")
-                    for _ in range(1 if args.single_stream else 2)]
+            bufs = [torch.zeros(F * H * W * ch, dtype=dt, device="cuda") for _ in range(n_streams["n"])]
             chunks = [(j, views[j:j + rt.abi.RT_MAX_BATCH]) for j in range(0, F, rt.abi.RT_MAX_BATCH)]
 
             def render(buf):
@@ -323,7 +327,7 @@ def main():
             # stream, so kernel_ms is each launch's own duration, overlap
             # included, as rocprofv3 reports it; the step time is shorter)
             return Plan(bufs, render, world * F * W * H, W * H * F // len(chunks), esize * ch, len(chunks),
-                        per_launch=not args.single_stream)
+                        per_launch=n_streams["n"] == 2)
         if mode == "spread":
             return spread_plan()
         n_frames = F if mode == "gather" else world * F
@@ -426,9 +430,9 @@ def main():
         ch, dt, _ = surface("rgba32f" if world == 1 else "rgb32f")
         view = rt.make_view(None, 0.0)
         if world == 1:
-            # consecutive steps on two streams and buffers (the next frame's
-            # launch under this one's last wave tiles) unless --single-stream
-            bufs = [torch.zeros(H * W * 4, dtype=dt, device="cuda") for _ in range(1 if args.single_stream else 2)]
+            # (with two streams: consecutive steps on two streams and buffers,
+            # the next frame's launch under this one's last wave tiles)
+            bufs = [torch.zeros(H * W * 4, dtype=dt, device="cuda") for _ in range(n_streams["n"])]
             return Plan(bufs, lambda buf: rt.render_device(ctx, scene, buf.data_ptr(), W, H, DEPTH, view=view,
                                                            stream=cur["s"].cuda_stream), W * H, W * H, 16)
         rows_mine = rt.shard_rows(H, BLOCK_ROWS, world, rank)
@@ -462,7 +466,7 @@ def main():
         freed = [None] * len(plan.bufs)  # event: the collective has finished reading bufs[slot]
 
         def step(timed, it):
-            if not plan.per_launch:  # frames rendered in place, launches back to back (--single-stream)
+            if not plan.per_launch:  # frames rendered in place, launches back to back (one stream)
                 plan.render(plan.bufs[0])
                 return
             slot = it % len(plan.bufs)
@@ -646,6 +650,20 @@ def main():
         extra["single_frame"] = {"frames_per_launch": 1, "us_per_frame": round(us, 3),
                                  "value": round(W * H / us, 3), "unit": "Mrays/s",
                                  "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
+    if world == 1 and not mc and n_streams["n"] == 1 and not args.no_pipelined:
+        # the same steps alternating between two render streams and buffers:
+        # a launch's last waves overlap the next step's launch (consecutive
+        # frames of a pipelined frame loop; every frame rendered in full).
+        # Its per-launch event spans include that overlap, so this rate
+        # carries no roofline of its own.
+        n_streams["n"] = 2
+        pp = batch_plan("none", "rgba32f") if batched else frame_plan()
+        ep, _, _ = measure(pp, args.steps, args.warmup)
+        extra["pipelined"] = {"value": round(pp.rays_per_step * args.steps / ep / 1e6, 3), "unit": "Mrays/s",
+                              "ms_per_step": round(ep / args.steps * 1e3, 5), "render_streams": 2,
+                              "note": "consecutive steps on two alternating streams and buffers"}
+        n_streams["n"] = 1
+        del pp
     if batched and world == 1 and rank == 0 and not args.no_rgba8:
         # the same F frames into the GL_RGBA8 surface the row-tiled N>1
         # steps write (main.cpp:223): the same-surface point of the 1..8-GPU
@@ -745,6 +763,7 @@ def main():
             "timing": {"per_rank": [{"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2]}
                                     for r, v in enumerate(per_rank)],
                        "collective": collective,
+                       "render_streams": n_streams["n"],
                        "note": "HIP events: kernel on the render stream, collective and assembly on the "
                                "collective stream, means over the timed steps"},
             "cpu_baseline": cpu,
