@@ -681,10 +681,17 @@ def main():
         del r8
     ms_per_step = elapsed / args.steps * 1e3
     value = plan.rays_per_step * args.steps / elapsed / 1e6
-    achieved = plan.px_per_launch * plan.bytes_per_pixel / (avg_kernel_ms * 1e-3) / 1e9
+    # time basis of the roofline: the kernel's own launch duration when each
+    # launch has the GPU alone (one render stream); with two overlapping
+    # render streams a launch's event span includes its neighbour's run, so
+    # the basis is the step: this GPU's stored bytes per step / step time
+    # (a lower bound on the kernel's rate; at one stream the two agree)
+    overlapped = n_streams["n"] == 2 and not mc
+    basis_ms = ms_per_step / plan.launches_per_step if overlapped else avg_kernel_ms
+    achieved = plan.px_per_launch * plan.bytes_per_pixel / (basis_ms * 1e-3) / 1e9
     # the same pixels at 16 B each (the float4 frame of the N=1 line): one
     # roofline scale for every point of a 1..8-GPU curve whatever its surface
-    achieved_f4 = plan.px_per_launch * 16 / (avg_kernel_ms * 1e-3) / 1e9
+    achieved_f4 = plan.px_per_launch * 16 / (basis_ms * 1e-3) / 1e9
     fpl = plan.px_per_launch // (W * H) if batched and world == 1 else 1
     build = rt.lib().rt_version().decode()
     pmc = pmc_latest(wl, fpl, build) if world == 1 else {}
@@ -758,6 +765,9 @@ def main():
                          "frac_float4_equivalent": round(achieved_f4 / HBM_PEAK_GBS, 5),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_ms, 5),
+                         "time_basis": ("step time per launch (two overlapping render streams: a launch's own "
+                                        "event span includes its neighbour's run)" if overlapped else
+                                        "kernel launch duration (HIP events, one render stream)"),
                          "bytes_per_launch": plan.px_per_launch * plan.bytes_per_pixel,
                          "valu": valu_bound(pmc, avg_kernel_ms)},
             "timing": {"per_rank": [{"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2]}
