@@ -5,10 +5,11 @@ Default workload (BASELINE.json configs[1]):
 materials, max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
 
 config2 (default). A step is F frames of the animated frame loop
-(main.cpp:81-86; --frames, default 8; frame k is the reference orbit camera at
-time k/60 s), rendered up to 8 frames per launch (rt_render_batch; SURVEY.md
-§8(f) row 3 — several frames per launch amortise the launch ramp-up and
-tail). The total work of a step is fixed: strong scaling.
+(main.cpp:81-86; --frames, default 64, about a second of the loop; frame k is
+the reference orbit camera at time k/60 s), rendered in one launch
+(rt_render_batch, up to 64 views; SURVEY.md §8(f) row 3 — several frames per
+launch amortise the launch's ramp-up, tail and dispatch gap, about 22 us per
+launch). The total work of a step is fixed: strong scaling.
   * N=1: every frame whole, float4 per pixel (16 B: the HBM-write roofline's
     bytes). The line also carries the one-frame-per-launch rate
     (`single_frame`, the shape of the reference's draw(), main.cpp:228-238),
@@ -104,8 +105,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
-    ap.add_argument("--frames", type=int, default=8,
-                    help="config2: animated frames per step, up to 8 per launch (rt_render_batch; "
+    ap.add_argument("--frames", type=int, default=64,
+                    help="config2: animated frames per step, up to 64 per launch (rt_render_batch; "
                          "SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
     ap.add_argument("--frame-exchange", choices=["spread", "gather", "all_to_all", "none"], default="spread",
                     help="config2 at N>1: spread (default) = every frame of the step row-tiled over the ranks, "

@@ -212,8 +212,11 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
 /* Several frames in one launch (the reference's frame loop, main.cpp:81-86,
  * batched): views[k] renders into out_device + k * rows * width * 4 floats,
  * where rows = height, or rt_shard_rows(...) when n_shards > 1 (each frame
- * then gets this shard's interleaved row blocks). The scene is shared. */
-#define RT_MAX_BATCH 8
+ * then gets this shard's interleaved row blocks). The scene is shared. Up to
+ * 8 views travel in the kernel arguments; 9..RT_MAX_BATCH views of a
+ * max_depth 0 or 1 frame go through a device buffer of the context (one
+ * launch), deeper ones run as launches of 8. */
+#define RT_MAX_BATCH 64
 int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views, int width,
                     int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
                     void *hip_stream);

@@ -146,7 +146,11 @@ struct FrameView {
     int32_t cull;      // 1: exactness-preserving culling enabled (consistent pinhole view)
     const void *blob;  // this view's scene blob (rt_render_batch_scenes); nullptr: LaunchParams::scene
 };
-constexpr int kMaxViews = 8;  // frames per launch (blockIdx.z)
+constexpr int kMaxViews = 8;  // frames per launch (blockIdx.z) with the views in the kernel arguments
+// Larger batches (up to RT_MAX_BATCH views, depth 0-1): the views and their
+// frame constants go to a per-context device buffer (one of kBatchSlots,
+// reused behind an event), read by render_kernel<D, false, true>.
+constexpr int kBatchSlots = 4;
 // per-frame constant records carried in the kernel arguments: all views'
 // (8 views of 16 spheres + 1 box = 264), at most kMaxViewConsts per view
 // (one record per thread of a work-group)
@@ -196,6 +200,11 @@ struct LaunchParams {
     // Rows [slice_begin, slice_begin + slice_rows) of the launch's local rows
     // (the whole launch when slice_rows = 0).
     int32_t slice_begin, slice_rows;
+    // > kMaxViews views (render_kernel<D, false, true>): n_views FrameViews
+    // and n_views x n_frame_consts records in device memory; nullptr: the
+    // arrays above
+    const FrameView *views_dev;
+    const float4 *consts_dev;
     float4 frame_consts[kMaxFrameConsts];
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
@@ -223,6 +232,14 @@ struct DeviceScene {
 // k * p.n_frame_consts, p.n_frame_consts = records per view, or 0 when they
 // do not all fit.
 void host_frame_setup(LaunchParams &p, const float4 *const *blobs);
+// One view's records for a device-side batch (render_batch_impl, > kMaxViews
+// views): writes 2 * n_spheres + n_boxes records of view V (p: the launch's
+// scene parameters) to out; the record count, or 0 if it exceeds
+// kMaxViewConsts (then every work-group derives them).
+int host_view_consts(const LaunchParams &p, const FrameView &V, const float4 *blob, float4 *out);
+// A view's kernel-side constants (unprojection, proj for culling, origin,
+// cull flag); false if its perspective divisions may not take the short form.
+bool fill_view(const rt_context *ctx, const rt_view &view, int width, int height, FrameView &out);
 
 // rt_camera.cpp: the reference orbit camera as llvmpipe evaluates it
 float gl_sin(float a);  // gallivm's polynomial sin / cos (run-time GLSL sin / cos)
@@ -268,6 +285,13 @@ struct rt_context {
     int timing = 1;   // RT_OPT_TIMING
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int host_consts = 1;  // RT_OPT_FRAME_CONSTS
+    // device-side view batches (> kMaxViews views): per slot a device buffer,
+    // its pinned host staging and an event after the last launch that read it
+    void *batch_dev[rtamd::kBatchSlots] = {};
+    void *batch_host[rtamd::kBatchSlots] = {};
+    hipEvent_t batch_done[rtamd::kBatchSlots] = {};
+    bool batch_used[rtamd::kBatchSlots] = {};
+    unsigned batch_next = 0;
     int n_cu = 0;               // compute units of the device
     int32_t *sched = nullptr;   // kSchedSlots x kSchedInts queue counters (zeroed)
     unsigned sched_next = 0;    // next slot: launches in flight on several streams use distinct slots

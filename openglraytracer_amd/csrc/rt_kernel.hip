@@ -1646,12 +1646,18 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 // 52 -> 67 us, 8-frame launches, tiled either way, 41.5 -> 50.6 us per frame)
 constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 
-template <int kDepth, bool kAccum>
+// kDev: a batch of more than kMaxViews views (depth 0-1): view z and its
+// frame constants come from the context's device buffer (p.views_dev,
+// p.consts_dev) instead of the kernel arguments; the view is read through
+// the constant address space (scalar loads, as the kernel arguments are).
+template <int kDepth, bool kAccum, bool kDev = false>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    const bool queued = kQueuedDepth(kDepth) && p.sched != nullptr;
+    const bool queued = kQueuedDepth(kDepth) && !kDev && p.sched != nullptr;
     const int z = queued ? 0 : static_cast<int>(blockIdx.z);
-    const FrameView &V = p.view[z];
+    FrameView Vdev;
+    if constexpr (kDev) Vdev = cload((const __attribute__((address_space(4))) FrameView *)(p.views_dev) + z);
+    const FrameView &V = kDev ? Vdev : p.view[z];
     // wave index through readfirstlane: provably wave-uniform to the compiler,
     // so the tile coordinates and culling rectangles stay in SGPRs
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1677,7 +1683,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // view's fit in the kernel arguments: host_frame_setup) — else derived
     // below by every work-group
     static_assert(kMaxViewConsts <= kThreads, "one record per thread");
-    if (tid < p.n_frame_consts) fc = p.frame_consts[z * p.n_frame_consts + tid];
+    if (tid < p.n_frame_consts) fc = (kDev ? p.consts_dev : p.frame_consts)[z * p.n_frame_consts + tid];
     float4 *sph_cam = lds + p.blob_units;
     int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
     float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
@@ -1793,10 +1799,10 @@ int groups_per_cu(const void *fn, size_t lds) {
     return n;
 }
 
-template <int kDepth, bool kAccum>
+template <int kDepth, bool kAccum, bool kDev = false>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
-    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum>);
+    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum, kDev>);
     dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, p.n_views);
     const int wave_tiles = ((p.width + 7) / 8) * ((p.slice_rows + 7) / 8);
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
@@ -1808,12 +1814,18 @@ hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     } else {
         p.sched = nullptr;
     }
-    hipLaunchKernelGGL((render_kernel<kDepth, kAccum>), grid, dim3(kThreads), lds, stream, p);
+    hipLaunchKernelGGL((render_kernel<kDepth, kAccum, kDev>), grid, dim3(kThreads), lds, stream, p);
     return hipGetLastError();
 }
 
 template <int kDepth>
 hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
+    if (p.views_dev) {  // a device-side view batch (render_batch_impl: depth 0-1, no accumulation)
+        if constexpr (kDepth <= 1) {
+            if (p.spp == 0) return launch_kernel<kDepth, false, true>(p, stream);
+        }
+        return hipErrorInvalidValue;
+    }
     return p.spp > 0 ? launch_kernel<kDepth, true>(p, stream) : launch_kernel<kDepth, false>(p, stream);
 }
 
@@ -1888,7 +1900,9 @@ hipError_t allow_large_lds(size_t bytes) {
 #define RT_KFN(d) reinterpret_cast<const void *>(&render_kernel<d, false>), \
                   reinterpret_cast<const void *>(&render_kernel<d, true>)
     const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
-                         RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9)};
+                         RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9),
+                         reinterpret_cast<const void *>(&render_kernel<0, false, true>),
+                         reinterpret_cast<const void *>(&render_kernel<1, false, true>)};
 #undef RT_KFN
     for (const void *f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));

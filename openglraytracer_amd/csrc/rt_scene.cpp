@@ -577,6 +577,13 @@ void host_frame_setup(LaunchParams &p, const float4 *const *blobs) {
     p.n_frame_consts = per;
 }
 
+int host_view_consts(const LaunchParams &p, const FrameView &V, const float4 *blob, float4 *out) {
+    const int per = 2 * p.n_spheres + p.n_boxes;
+    if (per == 0 || per > kMaxViewConsts || !blob) return 0;
+    view_frame_setup(p, V, blob, out);
+    return per;
+}
+
 // One view's records (host_frame_setup).
 static void view_frame_setup(const LaunchParams &p, const FrameView &V, const float4 *blob, float4 *out) {
     const int ns = p.n_spheres, nb = p.n_boxes;

@@ -172,6 +172,70 @@ def test_batched_frames_equal_single_frames(gpu_ctx, n_shards):
     sc.close()
 
 
+@pytest.mark.parametrize("depth,n_views,n_shards", [(0, 64, 1), (0, 23, 3), (1, 12, 1), (3, 19, 2)])
+def test_large_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
+    """More than 8 views in one rt_render_batch call: depth 0-1 in one launch
+    with the views and their frame constants in the context's device buffer
+    (render_kernel<D, false, true>), deeper frames as launches of 8 — each
+    frame bit-identical to its own single render (whole frames or one shard's
+    rows), with host frame constants and with device-derived ones, in the
+    float4 and the GL_RGBA8 surface; and, repeated, the slot ring is reused
+    behind its events."""
+    objs = scenes.bench_objects(16 if depth < 2 else 64)
+    w, h, block = 160, 90, 8
+    views = [rt.make_view(None, k / 60.0) for k in range(n_views)]
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        singles = [rt.render(gpu_ctx, sc, w, h, depth, view=v) for v in views]
+        for consts in (True, False):
+            gpu_ctx.set_host_frame_consts(consts)
+            for shard in range(n_shards):
+                rows = frame.shard_row_ids(h, block, n_shards, shard)
+                for rep in range(2 if consts else 1):
+                    out = dev_zeros((n_views, len(rows), w, 4), dtype=torch.float32, device="cuda")
+                    rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, views, block, n_shards, shard)
+                    got = out.cpu().numpy()
+                    for k in range(n_views):
+                        assert np.array_equal(got[k], singles[k][rows]), (consts, shard, rep, k)
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA8)
+        texels = dev_zeros((n_views, h, w), dtype=torch.int32, device="cuda")
+        rt.render_batch(gpu_ctx, sc, texels.data_ptr(), w, h, depth, views)
+        got8 = texels.cpu().numpy().view(np.uint8).reshape(n_views, h, w, 4)
+        for k in range(n_views):
+            assert np.array_equal(got8[k], rt.pack_rgba8(singles[k])), k
+    finally:
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA32F)
+        gpu_ctx.set_host_frame_consts(True)
+        sc.close()
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        with pytest.raises(rt.RTError) as e:
+            rt.render_batch(gpu_ctx, sc, 0, w, h, depth, (views * 7)[:rt.abi.RT_MAX_BATCH + 1])
+        assert e.value.code == rt.abi.RT_ERR_INVALID
+    finally:
+        sc.close()
+
+
+def test_large_animated_batch_of_scenes(gpu_ctx):
+    """rt_render_batch_scenes with 12 views (the device-buffer path): every
+    frame its own time-animated shipped scene (per-view blobs), equal to
+    single renders and to the oracle."""
+    times = [0.3 * k for k in range(12)]
+    w, h, depth = 64, 36, 1
+    scs = [rt.Scene(gpu_ctx, rt.reference_objects(t)) for t in times]
+    views = [rt.make_view(None, t) for t in times]
+    try:
+        out = dev_zeros((len(times), h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch_scenes(gpu_ctx, scs, out.data_ptr(), w, h, depth, views)
+        got = out.cpu().numpy()
+        for k, t in enumerate(times):
+            assert np.array_equal(got[k], rt.render(gpu_ctx, scs[k], w, h, depth, view=views[k])), k
+            assert np.array_equal(got[k], oracle_render(rt.reference_objects(t), w, h, depth, t)), k
+    finally:
+        for s in scs:
+            s.close()
+
+
 def _inside_sphere_camera():
     cam = rt.Camera()
     cam.position[:] = (-3.0, 4.0, 1.2)  # inside config 1's red-glass sphere (centre (-3, 4, 1), r 2)
