@@ -5,7 +5,7 @@
 The driver's 1/2/4/8-GPU scaling run (bench.py --gpus N, one rank per GPU,
 RCCL) cannot run on the one-GPU boxes of this pool. What a rank does per step
 can: for every N this renders each shard s of N exactly as rank s would —
-config 2: rt_render_batch of the step's 8 animated frames restricted to the
+config 2: rt_render_batch of the step's F animated frames restricted to the
 shard's interleaved 8-row blocks, into the GL_RGBA8 surface; config 4:
 rt_render_shard of the 7680x4320 frame into packed float3 — and times it with
 HIP events in sustained blocks (the max over shards is the step's critical
@@ -56,6 +56,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--workloads", default="config2,config4")
+    ap.add_argument("--frames", type=int, default=64, help="config 2: frames per step (bench.py --frames)")
     args = ap.parse_args()
     ns = [int(v) for v in args.ns.split(",")]
     ctx = rt.Context(0)
@@ -65,11 +66,11 @@ def main():
     sh = stream.cuda_stream
     for wl in args.workloads.split(","):
         if wl == "config2":
-            W, H, depth, nsph, F = 1920, 1080, 0, 16, 8
+            W, H, depth, nsph, F = 1920, 1080, 0, 16, args.frames
             ctx.set_output(rt.abi.RT_OUTPUT_RGBA8)
             ch, dt, bpp_send = 1, torch.int32, 3
             views = [rt.make_view(None, k / 60.0) for k in range(F)]
-            reps = 100
+            reps = max(10, 800 // F)
         else:
             W, H, depth, nsph, F = 7680, 4320, 4, 256, 1
             ctx.set_output(rt.abi.RT_OUTPUT_RGB32F)
