@@ -1364,10 +1364,20 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
     }
 }
 
+// Frame row of a launch's local row: the interleaved shard mapping (block
+// `blk` of this shard is block blk * n_shards + shard of the frame). A
+// power-of-two block (the bench's 8) takes shifts: the integer division it
+// replaces expands to a long VALU / SALU sequence, once per lane and eight
+// times per wave tile.
 __device__ __forceinline__ int output_row(const LaunchParams &p, int local) {
     if (p.n_shards <= 0) return p.row_begin + local;
-    const int blk = local / p.block_rows;
-    return (blk * p.n_shards + p.shard) * p.block_rows + (local - blk * p.block_rows);
+    const int b = p.block_rows;
+    if ((b & (b - 1)) == 0) {
+        const int sh = __builtin_ctz(static_cast<unsigned>(b));
+        return (((local >> sh) * p.n_shards + p.shard) << sh) + (local & (b - 1));
+    }
+    const int blk = local / b;
+    return (blk * p.n_shards + p.shard) * b + (local - blk * b);
 }
 
 // GL_RGBA8 unorm conversion as the reference's GL applies it: NaN -> 0,
@@ -1576,12 +1586,18 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
     const int lr0 = p.slice_begin + wy * 8;
     S.tx0 = wx * 8;
     S.tx1 = S.tx0 + 7;
-    S.ty0 = INT_MAX;
-    S.ty1 = INT_MIN;
-    for (int i = 0; i < 8; ++i) {
-        const int fy = output_row(p, lr0 + i);
-        S.ty0 = fy < S.ty0 ? fy : S.ty0;
-        S.ty1 = fy > S.ty1 ? fy : S.ty1;
+    if (p.n_shards <= 0 || (p.block_rows % 8 == 0 && lr0 % 8 == 0)) {
+        // the wave's 8 local rows lie in one block: 8 consecutive frame rows
+        S.ty0 = output_row(p, lr0);
+        S.ty1 = S.ty0 + 7;
+    } else {
+        S.ty0 = INT_MAX;
+        S.ty1 = INT_MIN;
+        for (int i = 0; i < 8; ++i) {
+            const int fy = output_row(p, lr0 + i);
+            S.ty0 = fy < S.ty0 ? fy : S.ty0;
+            S.ty1 = fy > S.ty1 ? fy : S.ty1;
+        }
     }
     float4 *out = p.out + static_cast<size_t>(z) * p.n_rows * p.width;
     const uint32_t idx = static_cast<uint32_t>(local_row) * static_cast<uint32_t>(p.width) + static_cast<uint32_t>(x);
