@@ -36,9 +36,16 @@ launch). The total work of a step is fixed: strong scaling.
     collective) and `verified`: the assembled frames of the last step equal
     the assembling rank's own whole-frame render byte for byte.
 
-config3 / config4 (3840x2160 / 64 spheres / depth 2, and
-7680x4320 / 256 spheres / depth 4 row-tiled across the GPUs with an RCCL
-gather). A step is ONE frame. N=1 renders it whole (float4). N>1: the frame's
+config3 at N=1 (3840x2160 / 64 spheres / depth 2): a step is
+F frames of the animated loop (--frames, default 7: the views one queued
+launch holds for this scene, every view's frame constants beside the scene
+in LDS), rendered in one rt_render_batch launch whose wave tiles are taken
+view after view from the queues, so the launch's tail is paid once per F
+frames; `single_frame` is the same frames one per launch.
+
+config3 at N>1 and config4 (7680x4320 / 256 spheres / depth 4 row-tiled across
+the GPUs with an RCCL gather): a step is ONE frame. N=1 renders it whole
+(float4; config 4's scene leaves LDS for one view per launch). N>1: the frame's
 interleaved 8-row blocks are dealt round-robin to the ranks (rt_render_shard,
 packed float3 shards), one RCCL gather brings the shards to rank 0 and rank 0
 de-interleaves them into the frame (frame.gather_frame); the gather of step i
@@ -105,9 +112,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
-    ap.add_argument("--frames", type=int, default=64,
-                    help="config2: animated frames per step, up to 64 per launch (rt_render_batch; "
-                         "SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="config2 (default 64) and config3 at N=1 (default 7): animated frames per step, up to "
+                         "64 per rt_render_batch call (SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
     ap.add_argument("--frame-exchange", choices=["spread", "gather", "all_to_all", "none"], default="spread",
                     help="config2 at N>1: spread (default) = every frame of the step row-tiled over the ranks, "
                          "frame k assembled on rank k %% N by one all-to-all (rank 0's xGMI ingress 1/N of the "
@@ -135,7 +142,7 @@ def parse():
     ap.add_argument("--no-rgba8", action="store_true",
                     help="config2 at N=1: skip the same-surface (GL_RGBA8) measurement")
     ap.add_argument("--no-single-frame", action="store_true",
-                    help="config2: skip the one-frame-per-launch measurement (profiling runs: one launch shape)")
+                    help="config2, config3 at N=1: skip the one-frame-per-launch measurement (profiling runs: one launch shape)")
     return ap.parse_args()
 
 
@@ -295,8 +302,8 @@ def main():
     assert sh, "need a non-default HIP stream"
     wl = args.workload
     mc = wl == "config5"
-    batched = wl == "config2"
-    F = args.frames
+    batched = wl == "config2" or (wl == "config3" and world == 1)
+    F = args.frames or (64 if wl == "config2" else 7)
     extra = {}
     surfaces = {"rgba32f": (rt.abi.RT_OUTPUT_RGBA32F, 4, torch.float32, "float4"),
                 "rgb32f": (rt.abi.RT_OUTPUT_RGB32F, 3, torch.float32, "packed float3 (alpha 0 dropped)"),
@@ -648,7 +655,7 @@ def main():
         e1.record(render_s)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n1 * 1e3
-        extra["single_frame"] = {"frames_per_launch": 1, "us_per_frame": round(us, 3),
+        extra["single_frame"] = {"frames_per_launch": 1, "us_per_frame": round(us, 3), "frames": "the step's F",
                                  "value": round(W * H / us, 3), "unit": "Mrays/s",
                                  "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
     if world == 1 and not mc and n_streams["n"] == 1 and not args.no_pipelined:
@@ -665,7 +672,7 @@ def main():
                               "note": "consecutive steps on two alternating streams and buffers"}
         n_streams["n"] = 1
         del pp
-    if batched and world == 1 and rank == 0 and not args.no_rgba8:
+    if batched and wl == "config2" and world == 1 and rank == 0 and not args.no_rgba8:
         # the same F frames into the GL_RGBA8 surface the row-tiled N>1
         # steps write (main.cpp:223): the same-surface point of the 1..8-GPU
         # curve, with its 4-B and its float4-equivalent roofline

@@ -156,6 +156,8 @@ constexpr int kBatchSlots = 4;
 // (one record per thread of a work-group)
 constexpr int kMaxFrameConsts = 272;
 constexpr int kMaxViewConsts = 256;
+// Largest LDS a work-group may request on gfx950 (160 KiB).
+constexpr size_t kMaxLds = 160 * 1024;
 
 struct LaunchParams {
     FrameView view[kMaxViews];
@@ -254,6 +256,10 @@ void reference_box_transforms(const float pos[3], const float ang[3], float l2w[
 // distribution (so the caller knows whether the counter slot is in use).
 hipError_t launch_render(LaunchParams &p, int max_depth, hipStream_t stream);
 size_t lds_bytes(const LaunchParams &p);
+// Views of one scene a queued launch at this depth holds (deep frames: every
+// view's per-frame constants beside the scene in LDS at the one-view
+// launch's occupancy), 1..kMaxViews; 1 below the queued depths.
+int queued_views(const LaunchParams &p, int max_depth);
 // Self-test of the kernel argument block on the context's stream (rt_create).
 int check_kernarg_block(hipStream_t stream);
 

@@ -1643,13 +1643,15 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 //    per kTileX x kTileY tile of a view (blockIdx.z), wave w rendering its
 //    8x8 quadrant; the scene and the view's per-frame constants are staged
 //    into LDS per work-group.
-//  * Queued (depth >= 2, one view, more wave tiles than resident waves,
-//    p.sched set): a grid of as many work-groups as are
-//    resident at once; each stages the scene and the per-frame constants
-//    once, then every wave renders 8x8 wave tiles on its own until the frame
-//    is done — no barrier after the prologue, and the frame ends on
-//    wave-tile granularity instead of with a tail of late work-groups. The
-//    wave tiles are dealt to kQueues queues by index (tile t in queue
+//  * Queued (depth >= 2, more wave tiles than resident waves, p.sched set,
+//    one scene): a grid of as many work-groups as are resident at once;
+//    each stages the scene and the per-frame constants of every view of the
+//    launch once, then every wave renders 8x8 wave tiles on its own until
+//    the launch is done — no barrier after the prologue, and the launch ends
+//    on wave-tile granularity instead of with a tail of late work-groups.
+//    Item t is wave tile t % T of view t / T (T tiles per view: the views
+//    in order, and one tail per launch instead of one per frame). The
+//    items are dealt to kQueues queues by index (item t in queue
 //    t % kQueues, spatially interleaved, so the queues carry equal work);
 //    global wave g belongs to queue g % kQueues, starts with tile g and then
 //    takes the queue's next tile from its atomic head, fetched one tile
@@ -1671,6 +1673,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     const bool queued = kQueuedDepth(kDepth) && !kDev && p.sched != nullptr;
     const int z = queued ? 0 : static_cast<int>(blockIdx.z);
+    const int n_staged = queued ? p.n_views : 1;  // views whose constants this work-group stages
     FrameView Vdev;
     if constexpr (kDev) Vdev = cload((const __attribute__((address_space(4))) FrameView *)(p.views_dev) + z);
     const FrameView &V = kDev ? Vdev : p.view[z];
@@ -1714,10 +1717,19 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     if (tid < p.blob_units) lds[tid] = first;
     RT_PHASE(11);
     for (int i = tid + kThreads; i < p.blob_units; i += kThreads) lds[i] = blob[i];
+    // (queued: view k's records at sph_cam + k * view_units)
+    const int view_units = 2 * p.n_spheres + p.n_boxes;
     if (p.n_frame_consts > 0) {
         if (tid < p.n_frame_consts) sph_cam[tid] = fc;
+        for (int i = tid + p.n_frame_consts; i < n_staged * p.n_frame_consts; i += kThreads)
+            sph_cam[i] = p.frame_consts[i];
     } else {
         frame_setup(p, V, sph_cam, sph_px, box_cam);
+        for (int k = 1; k < n_staged; ++k) {
+            float4 *c = sph_cam + k * view_units;
+            int4 *px = reinterpret_cast<int4 *>(c + p.n_spheres);
+            frame_setup(p, p.view[k], c, px, reinterpret_cast<float4 *>(px + p.n_spheres));
+        }
     }
     RT_PHASE(12);
 #ifdef RT_STATS
@@ -1758,7 +1770,8 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.nl = p.n_lights;
     S.nm = p.n_mats;
     const int wtx = (p.width + 7) / 8;
-    const int total = queued ? wtx * ((p.slice_rows + 7) / 8) : 1;
+    const int view_tiles = wtx * ((p.slice_rows + 7) / 8);
+    const int total = queued ? view_tiles * p.n_views : 1;
     const int g = static_cast<int>(blockIdx.x) * (kThreads / 64) + wave;  // global wave
     const int n_waves = static_cast<int>(gridDim.x) * (kThreads / 64);
     const int q = g % kQueues;
@@ -1773,9 +1786,17 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     while (t < total) {
         int nxt = 0;
         if (queued && lane == 0) nxt = atomicAdd(head, 1);  // fetched one tile ahead
-        const int wx = queued ? t % wtx : own_wx, wy = queued ? t / wtx : own_wy;
-        render_wave_tile<kDepth, kAccum>(p, S, V, wx, wy, z, queued ? wave_pixel(p, wx, wy) : own,
-                                              own_ray, !(queued || kAccum));
+        // (queued: the item's view and tile; t is wave-uniform)
+        const int zt = queued && p.n_views > 1 ? t / view_tiles : z, r = t - zt * view_tiles;
+        const int wx = queued ? r % wtx : own_wx, wy = queued ? r / wtx : own_wy;
+        Scene St = S;
+        if (queued && zt != 0) {
+            St.sph_cam = sph_cam + zt * view_units;
+            St.sph_px = reinterpret_cast<const int4 *>(St.sph_cam + p.n_spheres);
+            St.box_cam = reinterpret_cast<const float4 *>(St.sph_px + p.n_spheres);
+        }
+        render_wave_tile<kDepth, kAccum>(p, St, queued ? p.view[zt] : V, wx, wy, zt,
+                                              queued ? wave_pixel(p, wx, wy) : own, own_ray, !(queued || kAccum));
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
     RT_PHASE(7);
@@ -1815,18 +1836,56 @@ int groups_per_cu(const void *fn, size_t lds) {
     return n;
 }
 
+// LDS of a queued launch of n views: the scene and every view's per-frame
+// constants.
+size_t queued_lds_bytes(const LaunchParams &p, int n) {
+    return lds_bytes(p) + static_cast<size_t>(n - 1) * (2 * p.n_spheres + p.n_boxes) * sizeof(float4);
+}
+
+// Views of one scene a queued launch holds at the one-view launch's resident
+// work-groups per CU (their constants beside the scene in LDS), at most
+// kMaxViews (cached per kernel and scene shape: occupancy queries are host
+// work).
+int queued_views_for(const void *fn, const LaunchParams &p) {
+    struct Entry {
+        const void *fn;
+        size_t lds;
+        int units, n;
+    };
+    thread_local Entry cache[8] = {};
+    thread_local int next = 0;
+    const size_t lds = lds_bytes(p);
+    const int units = 2 * p.n_spheres + p.n_boxes;
+    for (const Entry &e : cache)
+        if (e.fn == fn && e.lds == lds && e.units == units && e.n > 0) return e.n;
+    const int g1 = groups_per_cu(fn, lds);
+    int n = 1;
+    while (n < kMaxViews && queued_lds_bytes(p, n + 1) <= kMaxLds &&
+           groups_per_cu(fn, queued_lds_bytes(p, n + 1)) >= g1)
+        ++n;
+    cache[next] = {fn, lds, units, n};
+    next = (next + 1) % 8;
+    return n;
+}
+
 template <int kDepth, bool kAccum, bool kDev = false>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
-    const size_t lds = lds_bytes(p);
+    size_t lds = lds_bytes(p);
     const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum, kDev>);
     dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, p.n_views);
-    const int wave_tiles = ((p.width + 7) / 8) * ((p.slice_rows + 7) / 8);
+    const int wave_tiles = ((p.width + 7) / 8) * ((p.slice_rows + 7) / 8) * p.n_views;
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
-    // queued: more wave tiles than resident waves, and every queue has a
-    // wave (a queue without one would leave its tiles unrendered)
-    if (kQueuedDepth(kDepth) && p.sched && p.n_views == 1 && wave_tiles > resident * (kThreads / 64) &&
-        resident * (kThreads / 64) >= kQueues) {
+    // queued: more wave tiles than resident waves, every queue has a wave (a
+    // queue without one would leave its tiles unrendered), and for several
+    // views: one scene (staged once) and every view's constants in LDS at the
+    // same resident work-groups (queued_views)
+    bool one_scene = p.n_views <= kMaxViews;
+    for (int k = 0; k < p.n_views && one_scene; ++k) one_scene = p.view[k].blob == nullptr;
+    if (kQueuedDepth(kDepth) && p.sched && wave_tiles > resident * (kThreads / 64) &&
+        resident * (kThreads / 64) >= kQueues &&
+        (p.n_views == 1 || (one_scene && queued_views_for(fn, p) >= p.n_views))) {
         grid = dim3(resident, 1, 1);
+        lds = queued_lds_bytes(p, p.n_views);
     } else {
         p.sched = nullptr;
     }
@@ -1850,6 +1909,23 @@ hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
 size_t lds_bytes(const LaunchParams &p) {
     // blob + per-sphere camera terms (16 B) and footprint (16 B) + per-box camera terms
     return (static_cast<size_t>(p.blob_units) + 2 * static_cast<size_t>(p.n_spheres) + p.n_boxes) * sizeof(float4);
+}
+
+int queued_views(const LaunchParams &p, int max_depth) {
+    const void *fn = nullptr;
+    switch (max_depth) {  // (the view-batch kernels: no accumulation)
+        case 2: fn = reinterpret_cast<const void *>(&render_kernel<2, false>); break;
+        case 3: fn = reinterpret_cast<const void *>(&render_kernel<3, false>); break;
+        case 4: fn = reinterpret_cast<const void *>(&render_kernel<4, false>); break;
+        case 5: fn = reinterpret_cast<const void *>(&render_kernel<5, false>); break;
+        case 6: fn = reinterpret_cast<const void *>(&render_kernel<6, false>); break;
+        case 7: fn = reinterpret_cast<const void *>(&render_kernel<7, false>); break;
+        case 8: fn = reinterpret_cast<const void *>(&render_kernel<8, false>); break;
+        case 9: fn = reinterpret_cast<const void *>(&render_kernel<9, false>); break;
+        default: return 1;
+    }
+    static_assert(!kQueuedDepth(1) && kQueuedDepth(2), "queued from depth 2");
+    return queued_views_for(fn, p);
 }
 
 hipError_t launch_render(LaunchParams &p, int max_depth, hipStream_t stream) {

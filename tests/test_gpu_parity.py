@@ -176,7 +176,7 @@ def test_batched_frames_equal_single_frames(gpu_ctx, n_shards):
 def test_large_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
     """More than 8 views in one rt_render_batch call: depth 0-1 in one launch
     with the views and their frame constants in the context's device buffer
-    (render_kernel<D, false, true>), deeper frames as launches of 8 — each
+    (render_kernel<D, false, true>), deeper frames as launches of at most 8 — each
     frame bit-identical to its own single render (whole frames or one shard's
     rows), with host frame constants and with device-derived ones, in the
     float4 and the GL_RGBA8 surface; and, repeated, the slot ring is reused
@@ -213,6 +213,42 @@ def test_large_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
             rt.render_batch(gpu_ctx, sc, 0, w, h, depth, (views * 7)[:rt.abi.RT_MAX_BATCH + 1])
         assert e.value.code == rt.abi.RT_ERR_INVALID
     finally:
+        sc.close()
+
+
+@pytest.mark.parametrize("depth,n_views,n_shards", [(2, 10, 1), (3, 2, 1), (2, 7, 2), (4, 3, 1)])
+def test_queued_view_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
+    """Deep batches large enough for the queued distribution (more wave tiles
+    than resident waves): one launch renders several views, every view's
+    frame constants beside the scene in LDS, the items view-major (and
+    batches beyond what one launch holds split into even launches) — each
+    frame bit-identical to its own single render, with host frame constants
+    (2 views of 64 spheres fit in the kernel arguments) and device-derived
+    ones, whole frames and shards, float4 and GL_RGBA8."""
+    objs = scenes.bench_objects(64)
+    w, h, block = 640, 360, 8
+    views = [rt.make_view(None, 0.5 + k / 30.0) for k in range(n_views)]
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        singles = [rt.render(gpu_ctx, sc, w, h, depth, view=v) for v in views]
+        for consts in (True, False):
+            gpu_ctx.set_host_frame_consts(consts)
+            for shard in range(n_shards):
+                rows = frame.shard_row_ids(h, block, n_shards, shard)
+                out = dev_zeros((n_views, len(rows), w, 4), dtype=torch.float32, device="cuda")
+                rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, views, block, n_shards, shard)
+                got = out.cpu().numpy()
+                for k in range(n_views):
+                    assert np.array_equal(got[k], singles[k][rows]), (consts, shard, k)
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA8)
+        texels = dev_zeros((n_views, h, w), dtype=torch.int32, device="cuda")
+        rt.render_batch(gpu_ctx, sc, texels.data_ptr(), w, h, depth, views)
+        got8 = texels.cpu().numpy().view(np.uint8).reshape(n_views, h, w, 4)
+        for k in range(n_views):
+            assert np.array_equal(got8[k], rt.pack_rgba8(singles[k])), k
+    finally:
+        gpu_ctx.set_output(rt.abi.RT_OUTPUT_RGBA32F)
+        gpu_ctx.set_host_frame_consts(True)
         sc.close()
 
 

@@ -22,7 +22,7 @@ if [ "$what" = prof ] || [ "$what" = all ]; then
   run prof_config2 900 tools/profile.sh $tag/c2 --steps 50 --warmup 5
   run prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
   run sum2 60 python tools/pmc_summary.py $out/c2 profiles/${tag}_config2 64 config2
-  run sum3 60 python tools/pmc_summary.py $out/c3 profiles/${tag}_config3 1 config3
+  run sum3 60 python tools/pmc_summary.py $out/c3 profiles/${tag}_config3 7 config3
   run sum4 60 python tools/pmc_summary.py $out/c4 profiles/${tag}_config4 1 config4
   run sum5 60 python tools/pmc_summary.py $out/c5 profiles/${tag}_config5 1 config5
   mkdir -p $out/profiles && cp profiles/${tag}_* profiles/pmc_*latest.json $out/profiles/
