@@ -73,3 +73,15 @@ print(f"mean wave-time before its first tile {ramp:.2f} us (start {start.mean():
       f"{(after_barrier - start).mean():.2f}); mean idle after its last tile {tail:.2f} us; "
       f"both as a share of the span: {(ramp + tail) / span:.3f}")
 print(f"per frame: span / views {span / n_views:.1f} us, lost wave-time per frame {(ramp + tail) / n_views:.1f} us")
+# per queue (global wave g serves queue g % 32): when its last wave ends —
+# the spread between queues is what sharing the queues' work at the end
+# (stealing) could recover; the spread inside a queue is tile granularity
+g = np.nonzero(live)[0]
+q = g % 32
+qend = np.array([end[q == k].max() for k in range(32)])
+qmean = np.array([end[q == k].mean() for k in range(32)])
+print("queue last end (us): min %.1f median %.1f max %.1f; queue mean wave end: min %.1f max %.1f"
+      % (qend.min(), np.median(qend), qend.max(), qmean.min(), qmean.max()))
+busy = (end - first_tile).sum()
+print("busy wave-time / waves = %.1f us (the span if every wave ended together); span %.1f us"
+      % (busy / len(end) + first_tile.mean(), span))
