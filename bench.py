@@ -655,9 +655,28 @@ def main():
         e1.record(render_s)
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n1 * 1e3
+        # the same launches alternating between two streams and two output
+        # buffers (a draw loop whose output image is double-buffered): frame
+        # k+1's launch fills the CUs that frame k's last waves leave idle
+        two = [one, torch.empty_like(one)]
+        s2 = [render_s, render_streams[1]]
+        e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e2.record(render_s)
+        s2[1].wait_event(e2)
+        for k in range(n1):
+            rt.render_batch(ctx, scene, two[k % 2].data_ptr(), W, H, DEPTH, [views1[k % F]],
+                            stream=s2[k % 2].cuda_stream)
+        render_s.wait_stream(s2[1])
+        e3.record(render_s)
+        torch.cuda.synchronize()
+        us2 = e2.elapsed_time(e3) / n1 * 1e3
         extra["single_frame"] = {"frames_per_launch": 1, "us_per_frame": round(us, 3), "frames": "the step's F",
                                  "value": round(W * H / us, 3), "unit": "Mrays/s",
-                                 "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
+                                 "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+                                 "two_streams": {"us_per_frame": round(us2, 3), "value": round(W * H / us2, 3),
+                                                 "note": "the same launches alternating between two streams "
+                                                         "and two output buffers"}}
+        del two
     if world == 1 and not mc and n_streams["n"] == 1 and not args.no_pipelined:
         # the same steps alternating between two render streams and buffers:
         # a launch's last waves overlap the next step's launch (consecutive

@@ -128,3 +128,23 @@ def test_pmc_summary_of_other_sources_is_not_reported(tmp_path, monkeypatch):
     assert "hbm_bytes_per_launch" not in other and other["stale_build"] == summary["build"]
     assert "stale_build" in bench.valu_bound(other, 10.0)
     assert bench.pmc_latest("config3", 1, summary["build"]) == {}
+
+
+@pytest.mark.gpu
+def test_config3_one_gpu_batches_frames():
+    """config3 at N=1: a step is F animated frames in one queued launch
+    (7 by default: the views one launch holds for this scene); the line
+    carries the one-frame-per-launch rate of the same frames, on one stream
+    and on two, and the two-stream step rate."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "config3", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    cfg = line["config"]
+    assert cfg["frames_per_step"] == 7 and cfg["frames_per_launch"] == 7 and cfg["max_depth"] == 2
+    assert line["roofline"]["bytes_per_launch"] == 7 * 3840 * 2160 * 16
+    one = line["single_frame"]
+    assert one["frames_per_launch"] == 1 and one["us_per_frame"] > 0 and one["two_streams"]["us_per_frame"] > 0
+    assert line["pipelined"]["render_streams"] == 2 and "rgba8_surface" not in line
