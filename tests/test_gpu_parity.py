@@ -216,17 +216,19 @@ def test_large_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
         sc.close()
 
 
-@pytest.mark.parametrize("depth,n_views,n_shards", [(2, 10, 1), (3, 2, 1), (2, 7, 2), (4, 3, 1)])
-def test_queued_view_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
+@pytest.mark.parametrize("depth,n_views,n_shards,w,h", [(2, 10, 1, 640, 360), (3, 2, 1, 640, 360),
+                                                        (2, 7, 2, 640, 360), (4, 3, 1, 640, 360),
+                                                        (3, 4, 3, 652, 366)])
+def test_queued_view_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards, w, h):
     """Deep batches large enough for the queued distribution (more wave tiles
     than resident waves): one launch renders several views, every view's
     frame constants beside the scene in LDS, the items view-major (and
     batches beyond what one launch holds split into even launches) — each
     frame bit-identical to its own single render, with host frame constants
     (2 views of 64 spheres fit in the kernel arguments) and device-derived
-    ones, whole frames and shards, float4 and GL_RGBA8."""
+    ones, whole frames and shards (ragged frames too), float4 and GL_RGBA8."""
     objs = scenes.bench_objects(64)
-    w, h, block = 640, 360, 8
+    block = 8
     views = [rt.make_view(None, 0.5 + k / 30.0) for k in range(n_views)]
     sc = rt.Scene(gpu_ctx, objs)
     try:
