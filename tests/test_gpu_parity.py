@@ -218,7 +218,7 @@ def test_large_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
 
 @pytest.mark.parametrize("depth,n_views,n_shards,w,h", [(2, 10, 1, 640, 360), (3, 2, 1, 640, 360),
                                                         (2, 7, 2, 640, 360), (4, 3, 1, 640, 360),
-                                                        (3, 4, 3, 652, 366)])
+                                                        (3, 7, 3, 652, 366)])
 def test_queued_view_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards, w, h):
     """Deep batches large enough for the queued distribution (more wave tiles
     than resident waves): one launch renders several views, every view's
