@@ -1639,7 +1639,8 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
 }
 
 // Work distribution.
-//  * Tiled (p.sched == nullptr, or a launch of several views): one work-group
+//  * Tiled (p.sched == nullptr: depth 0-1, views of several scenes, or too
+//    few wave tiles to fill the chip; launch_kernel decides): one work-group
 //    per kTileX x kTileY tile of a view (blockIdx.z), wave w rendering its
 //    8x8 quadrant; the scene and the view's per-frame constants are staged
 //    into LDS per work-group.
