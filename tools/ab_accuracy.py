@@ -3,7 +3,8 @@
     python tools/ab_accuracy.py BUILD [BUILD ...]
 
 BUILD as in tools/ab.py: a directory under _ab (tools/ablate.sh) or "main",
-optionally with context options (main:6=1 = RT_PRECISION_FAST). Every colour
+optionally with context options (main:1=0 = culling off; round 4 used it on the
+RT_FAST_* ablation builds of the price-of-exactness table). Every colour
 fixture of tests/golden (the reference's own shader on llvmpipe, configs 1-4
 and the shipped scene) is rendered through the drop-in call rt_render(cam =
 NULL, time) and compared per channel: max, p99 and mean |d|, pixels beyond
