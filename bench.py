@@ -5,9 +5,9 @@ Default workload (BASELINE.json configs[1]):
 materials, max_depth 0 (primary ray + shadow rays, raytrace_compute.glsl:325-405).
 
 config2 (default). A step is F frames of the animated frame loop
-(main.cpp:81-86; --frames, default 64, about a second of the loop; frame k is
+(main.cpp:81-86; --frames, default 256, about four seconds of the loop; frame k is
 the reference orbit camera at time k/60 s), rendered in one launch
-(rt_render_batch, up to 64 views; SURVEY.md §8(f) row 3 — several frames per
+(rt_render_batch, up to 256 views; SURVEY.md §8(f) row 3 — several frames per
 launch amortise the launch's ramp-up, tail and dispatch gap, about 22 us per
 launch). The total work of a step is fixed: strong scaling.
   * N=1: every frame whole, float4 per pixel (16 B: the HBM-write roofline's
@@ -113,8 +113,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
     ap.add_argument("--frames", type=int, default=None,
-                    help="config2 (default 64) and config3 at N=1 (default 7): animated frames per step, up to "
-                         "64 per rt_render_batch call (SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
+                    help="config2 (default 256) and config3 at N=1 (default 7): animated frames per step, up to "
+                         "256 per rt_render_batch call (SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
     ap.add_argument("--frame-exchange", choices=["spread", "gather", "all_to_all", "none"], default="spread",
                     help="config2 at N>1: spread (default) = every frame of the step row-tiled over the ranks, "
                          "frame k assembled on rank k %% N by one all-to-all (rank 0's xGMI ingress 1/N of the "
@@ -303,7 +303,7 @@ def main():
     wl = args.workload
     mc = wl == "config5"
     batched = wl == "config2" or (wl == "config3" and world == 1)
-    F = args.frames or (64 if wl == "config2" else 7)
+    F = args.frames or (256 if wl == "config2" else 7)
     extra = {}
     surfaces = {"rgba32f": (rt.abi.RT_OUTPUT_RGBA32F, 4, torch.float32, "float4"),
                 "rgb32f": (rt.abi.RT_OUTPUT_RGB32F, 3, torch.float32, "packed float3 (alpha 0 dropped)"),

@@ -218,7 +218,7 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
  * launch). Deeper frames run as even launches of as many views as one
  * launch holds beside the scene in GPU local memory (1..8, by the scene's
  * size: 7 for 64 spheres, 1 for 256). */
-#define RT_MAX_BATCH 64
+#define RT_MAX_BATCH 256
 int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views, int width,
                     int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
                     void *hip_stream);

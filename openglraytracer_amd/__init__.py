@@ -334,7 +334,7 @@ def render_device(ctx, scene, out_ptr, width, height, max_depth=0, view=None, ro
 
 def render_batch(ctx, scene, out_ptr, width, height, max_depth, views, block_rows=8, n_shards=1,
                  shard=0, stream=None):
-    """K frames (K = len(views) <= abi.RT_MAX_BATCH = 64) in one launch
+    """K frames (K = len(views) <= abi.RT_MAX_BATCH = 256) in one launch
     (depth 0-1; deeper frames in even queued launches of as many views as fit
     beside the scene in LDS, include/rt.h) into device memory laid out
     (K, rows, width, C) (C and dtype: the context's surface format); rows =

@@ -25,7 +25,7 @@ RT_OPT_FRAME_CONSTS = 4
 RT_OUTPUT_RGBA32F = 0
 RT_OUTPUT_RGBA8 = 1
 RT_OUTPUT_RGB32F = 2
-RT_MAX_BATCH = 64
+RT_MAX_BATCH = 256
 RT_MULTI_RCCL = 0
 RT_MULTI_COPY = 1
 

@@ -172,7 +172,7 @@ def test_batched_frames_equal_single_frames(gpu_ctx, n_shards):
     sc.close()
 
 
-@pytest.mark.parametrize("depth,n_views,n_shards", [(0, 64, 1), (0, 23, 3), (1, 12, 1), (3, 19, 2)])
+@pytest.mark.parametrize("depth,n_views,n_shards", [(0, 64, 1), (0, 23, 3), (1, 12, 1), (3, 19, 2), (0, 256, 2)])
 def test_large_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
     """More than 8 views in one rt_render_batch call: depth 0-1 in one launch
     with the views and their frame constants in the context's device buffer
@@ -210,7 +210,7 @@ def test_large_batches_equal_single_frames(gpu_ctx, depth, n_views, n_shards):
     sc = rt.Scene(gpu_ctx, objs)
     try:
         with pytest.raises(rt.RTError) as e:
-            rt.render_batch(gpu_ctx, sc, 0, w, h, depth, (views * 7)[:rt.abi.RT_MAX_BATCH + 1])
+            rt.render_batch(gpu_ctx, sc, 0, w, h, depth, (views * (rt.abi.RT_MAX_BATCH + 1))[:rt.abi.RT_MAX_BATCH + 1])
         assert e.value.code == rt.abi.RT_ERR_INVALID
     finally:
         sc.close()

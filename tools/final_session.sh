@@ -21,7 +21,7 @@ if [ "$what" = prof ] || [ "$what" = all ]; then
   run prof_config3 900 tools/profile.sh $tag/c3 --workload config3 --steps 10 --warmup 2
   run prof_config2 900 tools/profile.sh $tag/c2 --steps 50 --warmup 5
   run prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
-  run sum2 60 python tools/pmc_summary.py $out/c2 profiles/${tag}_config2 64 config2
+  run sum2 60 python tools/pmc_summary.py $out/c2 profiles/${tag}_config2 256 config2
   run sum3 60 python tools/pmc_summary.py $out/c3 profiles/${tag}_config3 7 config3
   run sum4 60 python tools/pmc_summary.py $out/c4 profiles/${tag}_config4 1 config4
   run sum5 60 python tools/pmc_summary.py $out/c5 profiles/${tag}_config5 1 config5
@@ -36,6 +36,6 @@ if [ "$what" = bench ] || [ "$what" = all ]; then
   # several ranks share the one GPU here (gloo): the step structure and the
   # byte-exact assembly, not scaling figures
   run gloo_config2_n4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
-      --master-port 29611 bench.py --gpus 4 --dist-backend gloo --steps 5 --warmup 2 --no-cpu-baseline
+      --master-port 29611 bench.py --gpus 4 --dist-backend gloo --steps 5 --warmup 2 --frames 64 --no-cpu-baseline
 fi
 echo done

@@ -56,3 +56,33 @@ e1.record(s)
 torch.cuda.synchronize()
 print("%s: direct C calls: host %.2f us per call, GPU %.2f us per frame"
       % (cfg, (t1 - t0) / n * 1e6, e0.elapsed_time(e1) / n * 1e3))
+
+# batches: host time per rt_render_batch call against its GPU time, whole
+# frames and one of 8 row-tiled shards (the config-2 step's launch at N = 8)
+if cfg == "config2":
+    big = torch.empty((64, h, w, 4), dtype=torch.float32, device="cuda")
+    for nv in (8, 64):
+        for shards in (1, 8):
+            vs = views[:nv]
+            for _ in range(3):
+                rt.render_batch(ctx, scene, big.data_ptr(), w, h, depth, vs, 8, shards, 0, stream=s.cuda_stream)
+            torch.cuda.synchronize()
+            reps = 40
+            e0.record(s)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                rt.render_batch(ctx, scene, big.data_ptr(), w, h, depth, vs, 8, shards, 0, stream=s.cuda_stream)
+            t1 = time.perf_counter()
+            e1.record(s)
+            torch.cuda.synchronize()
+            # the host's own cost: 3 calls from an idle GPU (fewer than the
+            # context's 4 batch slots, so no call waits for a slot to free)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            for _ in range(3):
+                rt.render_batch(ctx, scene, big.data_ptr(), w, h, depth, vs, 8, shards, 0, stream=s.cuda_stream)
+            t3 = time.perf_counter()
+            torch.cuda.synchronize()
+            print("%s: %d views, %d shard(s): back to back %.1f us per call on the host, GPU %.1f us per call; "
+                  "the host's own cost (3 calls, no slot wait) %.1f us per call"
+                  % (cfg, nv, shards, (t1 - t0) / reps * 1e6, e0.elapsed_time(e1) / reps * 1e3, (t3 - t2) / 3 * 1e6))

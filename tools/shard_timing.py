@@ -56,7 +56,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--workloads", default="config2,config4")
-    ap.add_argument("--frames", type=int, default=64, help="config 2: frames per step (bench.py --frames)")
+    ap.add_argument("--frames", type=int, default=256, help="config 2: frames per step (bench.py --frames)")
     args = ap.parse_args()
     ns = [int(v) for v in args.ns.split(",")]
     ctx = rt.Context(0)
