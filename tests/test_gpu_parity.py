@@ -942,6 +942,36 @@ def test_scene_used_on_more_than_eight_streams(gpu_ctx):
         assert np.array_equal(o.cpu().numpy(), want_b)
 
 
+def test_concurrent_batches_on_several_streams(gpu_ctx):
+    """Batches in flight together on three caller streams, none waiting for
+    another: queued deep batches (their queue-counter slots, kSchedSlots) and
+    depth-0 batches of more than 8 views (the device view ring, kBatchSlots),
+    several rounds, so every slot is reused while other launches run — each
+    frame bit-identical to its single render."""
+    objs = scenes.bench_objects(64)
+    w, h = 640, 360
+    views = [rt.make_view(None, 0.3 + k / 40.0) for k in range(12)]
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        want = {d: [rt.render(gpu_ctx, sc, w, h, d, view=v) for v in views] for d in (0, 2)}
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        jobs = []
+        for rnd in range(4):
+            for i, st in enumerate(streams):
+                depth = 2 if (rnd + i) % 2 == 0 else 0
+                nv = 5 if depth == 2 else 12
+                out = dev_zeros((nv, h, w, 4), dtype=torch.float32, device="cuda")
+                rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, views[:nv], stream=st.cuda_stream)
+                jobs.append((depth, nv, out))
+        torch.cuda.synchronize()
+        for depth, nv, out in jobs:
+            got = out.cpu().numpy()
+            for k in range(nv):
+                assert np.array_equal(got[k], want[depth][k]), (depth, k)
+    finally:
+        sc.close()
+
+
 STRAT = __import__("conftest").strat_manifest()
 
 
