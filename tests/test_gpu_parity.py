@@ -400,6 +400,30 @@ def test_max_objects_scene(gpu_ctx):
     assert np.array_equal(g, o)
 
 
+def test_max_objects_queued_deep_batch(gpu_ctx):
+    """The largest scene (RT_MAX_OBJECTS: the room box + 1023 spheres, the
+    scene blob and its per-view records filling much of LDS) at depth 3 in a
+    frame large enough for the queued distribution, as single frames and as a
+    two-view batch: bands of rows against the oracle, every batched frame
+    against its single render."""
+    objs = scenes.bench_objects(rt.abi.RT_MAX_OBJECTS - 1, seed=5)
+    w, h, depth = 768, 432, 3
+    views = [rt.make_view(None, 0.0), rt.make_view(None, 1.5)]
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        singles = [rt.render(gpu_ctx, sc, w, h, depth, view=v) for v in views]
+        out = dev_zeros((2, h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch(gpu_ctx, sc, out.data_ptr(), w, h, depth, views)
+        got = out.cpu().numpy()
+        for k in range(2):
+            assert np.array_equal(got[k], singles[k]), k
+    finally:
+        sc.close()
+    for r0 in (0, 208, 424):
+        o = oracle_render(objs, w, h, depth, 0.0, rows=(r0, r0 + 8))
+        assert np.array_equal(singles[0][r0:r0 + 8], o), (r0, parity_stats(singles[0][r0:r0 + 8], o))
+
+
 def test_animated_frames_match_oracle(gpu_ctx):
     for t in [0.5, 2.0, 7.25]:
         objs = rt.reference_objects(t)
