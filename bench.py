@@ -30,8 +30,11 @@ launch). The total work of a step is fixed: strong scaling.
     the gather-to-rank-0 shape link-bound at every N). --frame-exchange
     gather brings every frame to rank 0 (one contiguous buffer, one
     index_select); all_to_all keeps F frames per rank in flight (weak
-    scaling); none = independent whole frames. The exchange of step i
-    overlaps the render of step i+1 (double-buffered). The line also carries
+    scaling); none = independent whole frames. A step runs as four stages on
+    four streams — render, RGB8 packing, collective, de-interleave — so the
+    exchange of step i overlaps the render of step i+1 and the packing and
+    assembly of its neighbours (double-buffered), and a step costs its
+    longest stage rather than their sum. The line also carries
     `independent_frames` (every rank renders F whole frames of its own, no
     collective) and `verified`: the assembled frames of the last step equal
     the assembling rank's own whole-frame render byte for byte.
@@ -235,14 +238,18 @@ class Timer:
 
 class Plan:
     """One measured step shape: what a step renders (on the render stream),
-    how the shards are exchanged and assembled (on the collective stream)."""
+    how the shards are packed (pack stream), exchanged (collective stream) and
+    assembled (assembly stream): four stages on four streams, so step i's
+    exchange overlaps step i+1's render, step i+1's packing and step i-1's
+    assembly, and the step takes the longest stage, not their sum."""
 
     def __init__(self, bufs, render, rays_per_step, px_per_launch, bytes_per_pixel, launches_per_step=1,
-                 collective=None, assemble=None, per_launch=True):
+                 collective=None, assemble=None, per_launch=True, prepare=None):
         self.bufs = bufs
         self.render = render            # render(buf), asynchronous on the render stream
-        self.collective = collective    # collective(slot, src): on the collective stream after slot's render
-        self.assemble = assemble        # assemble(slot): on the collective stream after the collective
+        self.prepare = prepare          # prepare(slot, src): pack the shards to send (pack stream), or None
+        self.collective = collective    # collective(slot, src): on the collective stream after slot's packing
+        self.assemble = assemble        # assemble(slot): on the assembly stream after the collective
         self.rays_per_step = rays_per_step
         self.px_per_launch = px_per_launch
         self.bytes_per_pixel = bytes_per_pixel
@@ -297,6 +304,8 @@ def main():
     cur = {"s": render_s}
     n_streams = {"n": args.streams or (1 if world == 1 else 2)}  # read by the plan builders
     comm_s = torch.cuda.Stream()
+    pack_s = torch.cuda.Stream()  # N>1: the shards' RGB8 packing
+    asm_s = torch.cuda.Stream()  # N>1: the received frames' de-interleave
     torch.cuda.set_stream(comm_s)
     sh = render_s.cuda_stream
     assert sh, "need a non-default HIP stream"
@@ -364,8 +373,10 @@ def main():
                     if rank == 0 else None)
             idx = torch.as_tensor(frame.contiguous_assembly_rows(n_frames, H, BLOCK_ROWS, world), device=coll_dev)
 
-            def collective(slot, src):
+            def prepare(slot, src):
                 frame.pack_rgb8(src, sends[slot])
+
+            def collective(slot, src):
                 dist.gather(sends[slot], [bigs[slot][r * px * 3:(r + 1) * px * 3] for r in range(world)]
                             if rank == 0 else None, dst=0)  # RCCL: every shard to rank 0
 
@@ -374,6 +385,7 @@ def main():
                     return frame.assemble_contiguous(bigs[slot], n_frames, H, W, 3, idx)
                 return None
         elif mode == "gather":
+            prepare = None
             glists = ([[torch.empty(elems, dtype=dt, device=coll_dev) for _ in range(world)] for _ in bufs]
                       if rank == 0 else None)
             perm = torch.as_tensor(frame.assembly_permutation(H, BLOCK_ROWS, world), device=coll_dev)
@@ -386,6 +398,7 @@ def main():
                     return frame.assemble(glists[slot], n_frames, H, W, BLOCK_ROWS, channels=ch, perm=perm)
                 return None
         else:
+            prepare = None
             in_splits, out_splits = frame.exchange_splits(H, W, BLOCK_ROWS, world, rank, channels=ch,
                                                           frames_per_rank=F)
             recv = [torch.empty(sum(out_splits), dtype=dt, device=coll_dev) for _ in bufs]
@@ -397,7 +410,7 @@ def main():
             def assemble(slot):
                 return frame.assemble_frames(recv[slot], F, H, W, BLOCK_ROWS, world, channels=ch, idx=idx)
         return Plan(bufs, render, n_frames * W * H, W * rows_mine * n_frames // len(chunks), esize * ch,
-                    len(chunks), collective, assemble)
+                    len(chunks), collective, assemble, prepare=prepare)
 
     def spread_plan():
         """config2 at N>1, --frame-exchange spread (the default): the step's F
@@ -420,15 +433,18 @@ def main():
                 rt.render_batch(ctx, scene, buf.data_ptr() + 4 * j * frame_elems, W, H, DEPTH, vs,
                                 BLOCK_ROWS, world, rank, stream=cur["s"].cuda_stream)
 
-        def collective(slot, src):
+        def prepare(slot, src):
             frame.pack_rgb8(src, sends[slot])
+
+        def collective(slot, src):
             dist.all_to_all_single(recvs[slot], sends[slot], outs, ins)  # RCCL: frame k -> rank k % N
 
         def assemble(slot):
             if not mine:
                 return None
             return frame.assemble_frames(recvs[slot], len(mine), H, W, BLOCK_ROWS, world, channels=3, idx=idx)
-        plan = Plan(bufs, render, F * W * H, frame_elems * F // len(chunks), 4, len(chunks), collective, assemble)
+        plan = Plan(bufs, render, F * W * H, frame_elems * F // len(chunks), 4, len(chunks), collective, assemble,
+                    prepare=prepare)
         plan.mine = mine
         return plan
 
@@ -468,10 +484,13 @@ def main():
         elapsed seconds (max over ranks) and mean kernel / collective /
         assembly ms of every rank."""
         kt = Timer(torch, steps if plan.per_launch else 1)
+        pt = Timer(torch, steps)  # packing on pack_s
         ct = Timer(torch, steps)  # collective on comm_s
-        at = Timer(torch, steps)  # assembly on comm_s
+        at = Timer(torch, steps)  # assembly on asm_s (Monte-Carlo: the scaling, on comm_s)
         rendered = [torch.cuda.Event() for _ in plan.bufs]
-        freed = [None] * len(plan.bufs)  # event: the collective has finished reading bufs[slot]
+        freed = [None] * len(plan.bufs)  # event: bufs[slot] has been read (by the packing or the collective)
+        sent = [None] * len(plan.bufs)  # event: the collective has read the slot's send buffer
+        assembled = [None] * len(plan.bufs)  # event: the assembly has read the slot's receive buffer
 
         def step(timed, it):
             if not plan.per_launch:  # frames rendered in place, launches back to back (one stream)
@@ -481,7 +500,7 @@ def main():
             rs = render_streams[slot]
             cur["s"] = rs
             if freed[slot] is not None:
-                rs.wait_event(freed[slot])  # the collective of step it-2 has read bufs[slot]
+                rs.wait_event(freed[slot])  # step it-2's packing (or collective) has read bufs[slot]
             if timed:
                 kt.start(it, rs)
             plan.render(plan.bufs[slot])
@@ -490,20 +509,50 @@ def main():
             if plan.collective is None:
                 return
             rendered[slot].record(rs)
-            comm_s.wait_event(rendered[slot])
-            src = plan.bufs[slot] if coll_dev == "cuda" else plan.bufs[slot].cpu()
+            if plan.prepare is not None:
+                # packing on its own stream: the render buffer is free again
+                # once packed, and the collective stream carries only the
+                # transfer
+                pack_s.wait_event(rendered[slot])
+                if sent[slot] is not None:
+                    pack_s.wait_event(sent[slot])  # step it-2's collective has read the send buffer
+                with torch.cuda.stream(pack_s):
+                    src = plan.bufs[slot] if coll_dev == "cuda" else plan.bufs[slot].cpu()
+                    if timed:
+                        pt.start(it, pack_s)
+                    plan.prepare(slot, src)
+                    if timed:
+                        pt.stop(it, pack_s)
+                packed = torch.cuda.Event()
+                packed.record(pack_s)
+                freed[slot] = packed
+                comm_s.wait_event(packed)
+            else:
+                comm_s.wait_event(rendered[slot])
+                src = plan.bufs[slot] if coll_dev == "cuda" else plan.bufs[slot].cpu()
+            if assembled[slot] is not None:
+                comm_s.wait_event(assembled[slot])  # step it-2's assembly has read the receive buffer
             if timed:
                 ct.start(it, comm_s)
             plan.collective(slot, src)
             if timed:
                 ct.stop(it, comm_s)
-                at.start(it, comm_s)
-            plan.last = plan.assemble(slot)
-            if timed:
-                at.stop(it, comm_s)
-            e = torch.cuda.Event()
-            e.record(comm_s)
-            freed[slot] = e
+            done = torch.cuda.Event()
+            done.record(comm_s)
+            sent[slot] = done
+            if plan.prepare is None:
+                freed[slot] = done
+            # assembly on its own stream, beside the next step's transfer
+            asm_s.wait_event(done)
+            with torch.cuda.stream(asm_s):
+                if timed:
+                    at.start(it, asm_s)
+                plan.last = plan.assemble(slot)
+                if timed:
+                    at.stop(it, asm_s)
+            read = torch.cuda.Event()
+            read.record(asm_s)
+            assembled[slot] = read
 
         def mc_step(timed, it):
             accum.zero_()  # on comm_s: after the previous step's all-reduce read it
@@ -554,16 +603,17 @@ def main():
         exchanged = mc or plan.collective is not None
         cms = float(np.mean(ct.ms())) if exchanged else 0.0
         ams = float(np.mean(at.ms())) if exchanged else 0.0
+        pms = float(np.mean(pt.ms())) if plan.prepare is not None else 0.0
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-            mine = torch.tensor([kms, cms, ams], dtype=torch.float64, device=coll_dev)
+            mine = torch.tensor([kms, cms, ams, pms], dtype=torch.float64, device=coll_dev)
             every = [torch.zeros_like(mine) for _ in range(world)]
             dist.all_gather(every, mine)
             per_rank = [[round(float(v), 5) for v in e.cpu().tolist()] for e in every]
         else:
-            per_rank = [[round(kms, 5), round(cms, 5), round(ams, 5)]]
+            per_rank = [[round(kms, 5), round(cms, 5), round(ams, 5), round(pms, 5)]]
         return elapsed, kms, per_rank
 
     def verify(plan, n_frames, times, ch, dt, frames_of_rank=None):
@@ -797,12 +847,13 @@ def main():
                                         "kernel launch duration (HIP events, one render stream)"),
                          "bytes_per_launch": plan.px_per_launch * plan.bytes_per_pixel,
                          "valu": valu_bound(pmc, avg_kernel_ms)},
-            "timing": {"per_rank": [{"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2]}
-                                    for r, v in enumerate(per_rank)],
+            "timing": {"per_rank": [{"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2],
+                                     "pack_ms": v[3]} for r, v in enumerate(per_rank)],
                        "collective": collective,
                        "render_streams": n_streams["n"],
-                       "note": "HIP events: kernel on the render stream, collective and assembly on the "
-                               "collective stream, means over the timed steps"},
+                       "note": "HIP events, means over the timed steps: kernel on the render stream, packing, "
+                               "collective and assembly each on a stream of its own (the Monte-Carlo "
+                               "all-reduce and scaling on the collective stream)"},
             "cpu_baseline": cpu,
             "build": build,
         }
