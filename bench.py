@@ -81,6 +81,7 @@ configs' row subsets (oracle/cpu_baseline.py, child process, N=1 only).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config3|config4|config5]
 """
 import argparse
+import datetime
 import json
 import os
 import re
@@ -132,6 +133,8 @@ def parse():
                     help="N>1: skip checking the assembled frames against rank 0's whole-frame render")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="N>1: seconds after which a collective that cannot complete fails the rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0,
                     help="approximate budget of the llvmpipe baseline samples")
@@ -220,6 +223,74 @@ def valu_bound(pmc, kernel_ms):
     return out
 
 
+LINK_GBPS = (50.0, 100.0)  # per-direction rate RCCL may reach on one xGMI link (nominal ≈150 GB/s)
+
+
+def shard_timing():
+    """The committed per-rank timings of the N-GPU steps, measured on one GPU
+    (tools/shard_timing.py --out profiles/shard_timing_latest.json), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "shard_timing_latest.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def predict_step_ms(wl, world, mode, frames, rows_max, height, link_bytes_max, assembled_frames, spp_share=1.0):
+    """DESIGN.md §6's model of an N>1 step: render, RGB8 packing, collective
+    and de-interleave run on four streams, so a step takes its longest stage:
+    max(render, pack, busiest link bytes / B, assembly), for B in LINK_GBPS.
+    Render, packing and assembly times come from the committed one-GPU shard
+    timings (scaled to this step's frames; an N absent from them scales the
+    N=1 render by the shard's rows). Returns a dict, or None without data."""
+    st = shard_timing()
+    if st is None:
+        return None
+    recs = {r["n"]: r for r in st["records"] if r["workload"] == ("config2" if wl == "config2" else wl)}
+    if wl == "config5":
+        recs = {r["n"]: r for r in st["records"] if r["workload"] == "config2"}
+    if 1 not in recs:
+        return None
+    base = recs.get(world)
+    scale_f = frames / recs[1]["frames_per_step"]
+    if base is not None:
+        render = base.get("shard0_two_streams_ms", base["kernel_ms_max"]) * scale_f
+        src = "shard timing at N=%d" % world
+    else:
+        render = recs[1]["kernel_ms_max"] * scale_f * rows_max / height
+        src = "N=1 render x rows share (no shard timing at N=%d)" % world
+    if wl == "config5":
+        # the sample frames of config 2's scene: samples / frames of the N=1 step
+        render = recs[1]["kernel_ms_max"] / recs[1]["frames_per_step"] * spp_share
+        src = "config-2 frame time x samples of this rank"
+    near = base or recs[max(recs)]
+    pack = near.get("pack_rgb8_ms", 0.0) * scale_f * (near["n"] / world) if (wl == "config2" and mode in (
+        "spread", "gather")) else 0.0
+    asm = near.get("assembly_ms", 0.0) * assembled_frames / near["frames_per_step"] if near.get("assembly_ms") else 0.0
+    out = {"stages_ms": {"render": round(render, 4), "pack": round(pack, 4), "assembly": round(asm, 4)},
+           "busiest_link_bytes": int(link_bytes_max), "render_source": src,
+           "model": "max(render, pack, busiest link / B, assembly): four stages on four streams (DESIGN.md §6)",
+           "timings": "profiles/shard_timing_latest.json (%s)" % st.get("build", "?")}
+    for b in LINK_GBPS:
+        link = link_bytes_max / (b * 1e9) * 1e3
+        out["ms_per_step_B%d" % int(b)] = round(max(render, pack, link, asm), 4)
+        out["bound_B%d" % int(b)] = max([("render", render), ("pack", pack), ("link", link), ("assembly", asm)],
+                                        key=lambda kv: kv[1])[0]
+    return out
+
+
+def link_rate(v):
+    """A rank's achieved collective rates from [kernel, collective, assembly,
+    pack ms, busiest-link bytes, collective bytes]: bytes / the collective's
+    HIP-event time (which includes waiting for the slowest peer, so a lower
+    bound on what the links carry)."""
+    if len(v) < 6 or not v[4] or v[1] <= 0:
+        return {}
+    return {"link_bytes": int(v[4]), "collective_bytes": int(v[5]),
+            "link_GBps": round(v[4] / (v[1] * 1e-3) / 1e9, 3),
+            "collective_GBps": round(v[5] / (v[1] * 1e-3) / 1e9, 3)}
+
+
 class Timer:
     """HIP event pairs on a stream; mean milliseconds per recorded pair."""
 
@@ -257,6 +328,15 @@ class Plan:
         # one kernel event pair per step (else one pair around the timed region)
         self.per_launch = per_launch or collective is not None
         self.last = None                # assembled output of the last step (assemble's return value)
+        # this rank's collective bytes per step: over its busiest peer link
+        # (sent or received) and in total (sent + received, other ranks only)
+        self.link_bytes = 0
+        self.coll_bytes = 0
+
+    def set_link(self, sent, received):
+        """sent[p] / received[p]: bytes to / from rank p this step (own rank 0)."""
+        self.link_bytes = max([max(a, b) for a, b in zip(sent, received)] + [0])
+        self.coll_bytes = sum(sent) + sum(received)
 
 
 def main():
@@ -274,15 +354,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
-    device = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(device)
+    device = local % max(1, torch.cuda.device_count())  # (counting devices does not initialise the GPU)
     coll_dev = "cuda"
     if world > 1:
+        # a collective that cannot complete (a peer gone, RCCL failing) raises
+        # within --collective-timeout; guarded() turns it into a nonzero exit
+        # of this rank (an RCCL error aborts the frame)
+        timeout = datetime.timedelta(seconds=args.collective_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            torch.cuda.set_device(device)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device), timeout=timeout)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=timeout)
             coll_dev = "cpu"
+        inject_fault(rank, "init")
+        dist.barrier()  # every rank is up before any GPU work
+    torch.cuda.set_device(device)
 
     ctx = rt.Context(device)
     scene = rt.Scene(ctx, rt.bench_objects(cfg["spheres"], 0))
@@ -343,7 +430,10 @@ def main():
             # (two streams: an event pair around every step's launches on its
             # stream, so kernel_ms is each launch's own duration, overlap
             # included, as rocprofv3 reports it; the step time is shorter)
-            return Plan(bufs, render, world * F * W * H, W * H * F // len(chunks), esize * ch, len(chunks),
+            # kernel launches per step: the library splits a deep batch into
+            # queued launches of as many views as fit beside the scene in LDS
+            launches = sum(rt.batch_launches(ctx, scene, len(vs), DEPTH) for _, vs in chunks)
+            return Plan(bufs, render, world * F * W * H, W * H * F // launches, esize * ch, launches,
                         per_launch=n_streams["n"] == 2)
         if mode == "spread":
             return spread_plan()
@@ -409,8 +499,18 @@ def main():
 
             def assemble(slot):
                 return frame.assemble_frames(recv[slot], F, H, W, BLOCK_ROWS, world, channels=ch, idx=idx)
-        return Plan(bufs, render, n_frames * W * H, W * rows_mine * n_frames // len(chunks), esize * ch,
+        plan = Plan(bufs, render, n_frames * W * H, W * rows_mine * n_frames // len(chunks), esize * ch,
                     len(chunks), collective, assemble, prepare=prepare)
+        if mode == "gather":
+            # every rank's equal-size flat shard buffer to rank 0 (RGB8: 3 B
+            # per pixel; else the surface's elements)
+            per = 3 * frame.flat_shard_elems(n_frames, H, W, BLOCK_ROWS, world, 1) if surf == "rgba8" else esize * elems
+            plan.set_link([per if (rank != 0 and p == 0) else 0 for p in range(world)],
+                          [per if (rank == 0 and p != 0) else 0 for p in range(world)])
+        else:
+            plan.set_link([esize * v if p != rank else 0 for p, v in enumerate(in_splits)],
+                          [esize * v if p != rank else 0 for p, v in enumerate(out_splits)])
+        return plan
 
     def spread_plan():
         """config2 at N>1, --frame-exchange spread (the default): the step's F
@@ -446,6 +546,8 @@ def main():
         plan = Plan(bufs, render, F * W * H, frame_elems * F // len(chunks), 4, len(chunks), collective, assemble,
                     prepare=prepare)
         plan.mine = mine
+        plan.set_link([v if p != rank else 0 for p, v in enumerate(ins)],
+                      [v if p != rank else 0 for p, v in enumerate(outs)])
         return plan
 
     def frame_plan():
@@ -475,9 +577,13 @@ def main():
             if rank == 0:
                 return frame.assemble_contiguous(bigs[slot], 1, H, W, ch, idx)
             return None
-        return Plan(bufs, lambda buf: rt.render_shard(ctx, scene, buf.data_ptr(), W, H, DEPTH, BLOCK_ROWS, world,
+        plan = Plan(bufs, lambda buf: rt.render_shard(ctx, scene, buf.data_ptr(), W, H, DEPTH, BLOCK_ROWS, world,
                                                       rank, view=view, stream=cur["s"].cuda_stream),
                     W * H, W * rows_mine, 4 * ch, 1, collective, assemble)
+        per = 4 * elems  # every rank's flat float3 shard buffer to rank 0
+        plan.set_link([per if (rank != 0 and p == 0) else 0 for p in range(world)],
+                      [per if (rank == 0 and p != 0) else 0 for p in range(world)])
+        return plan
 
     def measure(plan, steps, warmup):
         """Warm-up, then `steps` timed steps between barriers; returns the
@@ -492,12 +598,18 @@ def main():
         sent = [None] * len(plan.bufs)  # event: the collective has read the slot's send buffer
         assembled = [None] * len(plan.bufs)  # event: the assembly has read the slot's receive buffer
 
+        # one-stream plans launch on render_s, where their event pair is
+        # recorded (a previous two-stream measurement may have left cur["s"]
+        # on the other render stream)
+        cur["s"] = render_s
+
         def step(timed, it):
             if not plan.per_launch:  # frames rendered in place, launches back to back (one stream)
                 plan.render(plan.bufs[0])
                 return
             slot = it % len(plan.bufs)
-            rs = render_streams[slot]
+            # (--streams 1 at N>1: both buffer slots on render_s)
+            rs = render_streams[slot % n_streams["n"]]
             cur["s"] = rs
             if freed[slot] is not None:
                 rs.wait_event(freed[slot])  # step it-2's packing (or collective) has read bufs[slot]
@@ -532,6 +644,8 @@ def main():
                 src = plan.bufs[slot] if coll_dev == "cuda" else plan.bufs[slot].cpu()
             if assembled[slot] is not None:
                 comm_s.wait_event(assembled[slot])  # step it-2's assembly has read the receive buffer
+            if timed and it == 0:
+                inject_fault(rank, "step")
             if timed:
                 ct.start(it, comm_s)
             plan.collective(slot, src)
@@ -588,11 +702,11 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if not plan.per_launch:
-            kt.start(0, render_s)
+            kt.start(0, cur["s"])
         for it in range(steps):
             run(True, it)
         if not plan.per_launch:
-            kt.stop(0, render_s)
+            kt.stop(0, cur["s"])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -608,12 +722,13 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-            mine = torch.tensor([kms, cms, ams, pms], dtype=torch.float64, device=coll_dev)
+            mine = torch.tensor([kms, cms, ams, pms, plan.link_bytes, plan.coll_bytes], dtype=torch.float64,
+                                device=coll_dev)
             every = [torch.zeros_like(mine) for _ in range(world)]
             dist.all_gather(every, mine)
             per_rank = [[round(float(v), 5) for v in e.cpu().tolist()] for e in every]
         else:
-            per_rank = [[round(kms, 5), round(cms, 5), round(ams, 5), round(pms, 5)]]
+            per_rank = [[round(kms, 5), round(cms, 5), round(ams, 5), round(pms, 5), 0, 0]]
         return elapsed, kms, per_rank
 
     def verify(plan, n_frames, times, ch, dt, frames_of_rank=None):
@@ -646,6 +761,20 @@ def main():
         return {"frames_checked": px // (H * W), "pixels": px, "mismatched_pixels": bad, "bit_exact": bad == 0,
                 "against": "the assembling rank's own whole-frame render of the same frames, same surface"}
 
+    def verify_n1(buf, frames, ch, dt):
+        torch.cuda.synchronize()
+        one = torch.empty((H, W, ch), dtype=dt, device="cuda")
+        got_all = buf.view(dt).reshape(-1, H, W, ch)
+        bad = 0
+        for k in frames:
+            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [rt.make_view(None, frame_time(k))])  # synchronous
+            diff = got_all[k].view(torch.int32) != one.view(torch.int32)
+            bad += int(diff.reshape(H * W, -1).any(-1).sum().item())
+        return {"frames_checked": frames, "pixels": len(frames) * H * W, "mismatched_pixels": bad,
+                "bit_exact": bad == 0,
+                "against": "single-frame renders of the same views (one view per launch, the draw() shape), "
+                           "compared as bytes"}
+
     view = None
     if batched:
         mode = args.frame_exchange if world > 1 else "none"
@@ -660,11 +789,25 @@ def main():
         sample0 = rank * (spp // world) + min(rank, spp % world)
         accum = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
         plan = Plan([accum], None, spp * W * H, W * H, 16)
+        if world > 1:
+            # a ring all-reduce moves 2 (N-1)/N of the buffer over each link
+            # in each direction (RCCL's choice of algorithm may differ)
+            ring = int(2 * (world - 1) / world * H * W * 16)
+            nxt, prv = (rank + 1) % world, (rank - 1) % world
+            plan.set_link([ring if p == nxt else 0 for p in range(world)],
+                          [ring if p == prv else 0 for p in range(world)])
     else:
         plan = frame_plan()
 
     elapsed, avg_kernel_ms, per_rank = measure(plan, args.steps, args.warmup)
     verified = None
+    if batched and world == 1 and not args.no_verify:
+        # N=1: frames of the last timed step (the first, middle and last of
+        # the F) against single renders of the same views — one view per
+        # launch, the draw() shape (main.cpp:228-238), a kernel instance of
+        # its own — byte for byte (raytrace_compute.glsl:404)
+        last = plan.bufs[(args.steps - 1) % len(plan.bufs) if plan.per_launch else 0]
+        verified = verify_n1(last, sorted({0, (F - 1) // 2, F - 1}), surfaces[surf][1], surfaces[surf][2])
     if world > 1 and not args.no_verify and not mc:
         if batched and mode == "gather":
             verified = verify(plan, F, [frame_time(k) for k in range(F)], surfaces[surf][1], surfaces[surf][2])
@@ -695,37 +838,54 @@ def main():
         # main.cpp:210-238): K launches back to back, one event pair
         n1 = max(20, args.steps)
         one = torch.empty(H * W * 4, dtype=torch.float32, device="cuda")
-        views1 = [rt.make_view(None, frame_time(k)) for k in range(F)]
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for k in range(3):
-            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views1[k % F]], stream=sh)
-        e0.record(render_s)
-        for k in range(n1):
-            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views1[k % F]], stream=sh)
-        e1.record(render_s)
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / n1 * 1e3
-        # the same launches alternating between two streams and two output
-        # buffers (a draw loop whose output image is double-buffered): frame
-        # k+1's launch fills the CUs that frame k's last waves leave idle
         two = [one, torch.empty_like(one)]
+        views1 = [rt.make_view(None, frame_time(k)) for k in range(F)]
         s2 = [render_s, render_streams[1]]
-        e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e2.record(render_s)
-        s2[1].wait_event(e2)
-        for k in range(n1):
+
+        def one_stream():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(render_s)
+            for k in range(n1):
+                rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views1[k % F]], stream=sh)
+            e1.record(render_s)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / n1 * 1e3
+
+        def two_streams():
+            # the same launches alternating between two streams and two
+            # output buffers (a draw loop whose output image is
+            # double-buffered): frame k+1's launch may fill the CUs that
+            # frame k's last waves leave idle
+            e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e2.record(render_s)
+            s2[1].wait_event(e2)
+            for k in range(n1):
+                rt.render_batch(ctx, scene, two[k % 2].data_ptr(), W, H, DEPTH, [views1[k % F]],
+                                stream=s2[k % 2].cuda_stream)
+            render_s.wait_stream(s2[1])
+            e3.record(render_s)
+            torch.cuda.synchronize()
+            return e2.elapsed_time(e3) / n1 * 1e3
+        # both shapes warmed on both streams, then 3 interleaved repeats each
+        # (the chip's clock drifts with load): medians and spreads
+        for k in range(4):
             rt.render_batch(ctx, scene, two[k % 2].data_ptr(), W, H, DEPTH, [views1[k % F]],
                             stream=s2[k % 2].cuda_stream)
-        render_s.wait_stream(s2[1])
-        e3.record(render_s)
         torch.cuda.synchronize()
-        us2 = e2.elapsed_time(e3) / n1 * 1e3
+        ones, twos = [], []
+        for _ in range(3):
+            ones.append(one_stream())
+            twos.append(two_streams())
+        us, us2 = float(np.median(ones)), float(np.median(twos))
         extra["single_frame"] = {"frames_per_launch": 1, "us_per_frame": round(us, 3), "frames": "the step's F",
                                  "value": round(W * H / us, 3), "unit": "Mrays/s",
+                                 "repeats_us": [round(v, 3) for v in ones],
                                  "roofline_frac": round(W * H * 16 / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
                                  "two_streams": {"us_per_frame": round(us2, 3), "value": round(W * H / us2, 3),
+                                                 "repeats_us": [round(v, 3) for v in twos],
                                                  "note": "the same launches alternating between two streams "
-                                                         "and two output buffers"}}
+                                                         "and two output buffers; median of 3 repeats "
+                                                         "interleaved with the one-stream ones"}}
         del two
     if world == 1 and not mc and n_streams["n"] == 1 and not args.no_pipelined:
         # the same steps alternating between two render streams and buffers:
@@ -847,8 +1007,8 @@ def main():
                                         "kernel launch duration (HIP events, one render stream)"),
                          "bytes_per_launch": plan.px_per_launch * plan.bytes_per_pixel,
                          "valu": valu_bound(pmc, avg_kernel_ms)},
-            "timing": {"per_rank": [{"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2],
-                                     "pack_ms": v[3]} for r, v in enumerate(per_rank)],
+            "timing": {"per_rank": [dict({"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2],
+                                          "pack_ms": v[3]}, **link_rate(v)) for r, v in enumerate(per_rank)],
                        "collective": collective,
                        "render_streams": n_streams["n"],
                        "note": "HIP events, means over the timed steps: kernel on the render stream, packing, "
@@ -862,6 +1022,24 @@ def main():
                                                                                       pmc["stale_build"])
         if verified is not None:
             line["verified"] = verified
+        if world > 1:
+            # DESIGN.md §6's prediction of this step from the committed
+            # one-GPU shard timings, beside the measured ms_per_step
+            if batched:
+                m = mode
+                assembled = {"spread": -(-F // world), "gather": F, "all_to_all": F}.get(mode, 0)
+                frames_step = F if mode in ("spread", "gather") else world * F
+                # frames whose shards (whole frames for `none`) a rank renders per step
+                frames_rank = world * F if mode == "all_to_all" else F
+            else:
+                m, assembled, frames_step, frames_rank = ("allreduce" if mc else "gather"), (0 if mc else 1), 1, 1
+            pred = predict_step_ms(wl, world, m, frames_rank, rt.shard_rows(H, BLOCK_ROWS, world, 0), H,
+                                   max(v[4] for v in per_rank), assembled,
+                                   spp_share=(-(-cfg.get("spp", 1) // world)) if mc else 1.0)
+            if pred is not None and not (batched and mode == "none"):
+                pred["measured_ms_per_step"] = round(ms_per_step, 5)
+                pred["frames_per_step"] = frames_step
+                line["predicted_ms_per_step"] = pred
         line.update(extra)
         print(json.dumps(line), flush=True)
     scene.close()
@@ -872,5 +1050,40 @@ def main():
         raise SystemExit("assembled frames differ from the whole-frame render on %d pixels"
                          % verified["mismatched_pixels"])
 
+EXIT_RANK_FAILED = 17  # this rank's step failed (a collective, a render, a check)
+EXIT_FAULT_INJECTED = 3
+
+
+def inject_fault(rank, stage):
+    """Test hook (tests/test_bench.py): RT_BENCH_FAULT='<rank>:<stage>' makes
+    that rank exit at once, without a word to its peers, at `stage` ('init':
+    after joining the group; 'step': before its first timed collective) — a
+    rank that dies mid-frame."""
+    spec = os.environ.get("RT_BENCH_FAULT", "")
+    if spec and spec == "%d:%s" % (rank, stage):
+        sys.stderr.write("bench.py rank %d: injected fault at %s, exiting\n" % (rank, stage))
+        sys.stderr.flush()
+        os._exit(EXIT_FAULT_INJECTED)
+
+
+def guarded(fn):
+    """Run the bench; at N>1 any failure (a collective that errors or times
+    out because a peer is gone, an RCCL error, a failed render) aborts this
+    rank's frame with a message and a nonzero exit, without the process
+    group's teardown, which would wait for the missing peer."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return fn()
+    try:
+        return fn()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 — every failure ends the rank
+        sys.stderr.write("bench.py rank %s: step failed, aborting the frame: %s: %s\n"
+                         % (os.environ.get("RANK", "?"), type(e).__name__, str(e)[:500]))
+        sys.stderr.flush()
+        os._exit(EXIT_RANK_FAILED)
+
+
 if __name__ == "__main__":
-    main()
+    guarded(main)

@@ -189,8 +189,14 @@ int rt_scene_update(rt_context *ctx, rt_scene *scene, const rt_object *objs, int
  *             context's GPU if out_is_device, else host memory.
  *  hip_stream hipStream_t; NULL = the context's own stream and the call
  *             returns after the frame is complete (the reference's glFinish,
- *             main.cpp:238). A non-NULL stream makes the call asynchronous
- *             (out_is_device must then be 1).
+ *             main.cpp:238). That stream is a blocking HIP stream: the
+ *             render starts after all work queued earlier on the device's
+ *             null stream (torch's default stream, e.g. a fill of `out`), as
+ *             glDispatchCompute follows the earlier commands of its context
+ *             (main.cpp:220-238). A non-NULL stream makes the call
+ *             asynchronous and ordered only on that stream (out_is_device
+ *             must then be 1). Every render entry point below treats
+ *             hip_stream the same way.
  * No allocation happens here after the first call at a given size. */
 int rt_render(rt_context *ctx, const rt_scene *scene, const rt_camera *cam, float time, int width,
               int height, int max_depth, int row_begin, int row_end, float *out, int out_is_device,
@@ -219,6 +225,11 @@ int rt_render_shard(rt_context *ctx, const rt_scene *scene, const rt_view *view,
  * launch holds beside the scene in GPU local memory (1..8, by the scene's
  * size: 7 for 64 spheres, 1 for 256). */
 #define RT_MAX_BATCH 256
+/* The number of kernel launches rt_render_batch makes for n_views views of
+ * this scene at max_depth (1 up to RT_MAX_BATCH views at depth 0-1; deep
+ * batches: ceil(n_views / views per queued launch)), or a negative RT_ERR_*.
+ * No GPU work; for callers that time or size per launch. */
+int rt_batch_launches(rt_context *ctx, const rt_scene *scene, int n_views, int max_depth);
 int rt_render_batch(rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views, int width,
                     int height, int max_depth, int block_rows, int n_shards, int shard, float *out_device,
                     void *hip_stream);
@@ -240,7 +251,9 @@ int rt_render_batch_scenes(rt_context *ctx, const rt_scene *const *scenes, const
  * pixel (x, y) is the reference ray through NDC ((x - W/2 + jx) / (W/2),
  * (y - H/2 + jy) / (H/2)) with (jx, jy) in [0, 1)^2 from a counter-based hash
  * of (seed, s, y*W + x) when jitter != 0, else (0, 0) (then every sample
- * equals the reference frame). The mean is accum / total samples. Disjoint
+ * equals the reference frame). With hip_stream NULL a zero fill queued on
+ * the null stream (torch's default stream) is complete before the
+ * accumulation reads the buffer. The mean is accum / total samples. Disjoint
  * sample ranges on several GPUs sum (RCCL all-reduce) to the same estimate
  * up to float re-association. */
 int rt_render_accumulate(rt_context *ctx, const rt_scene *scene, const rt_view *view, int width, int height,
@@ -314,7 +327,8 @@ int rt_multi_last_ms(rt_multi *m, float *kernel_ms, float *gather_ms, float *ass
 int rt_context_set(rt_context *ctx, int option, int value);
 
 /* Kernel-only timing of the last render call (ms, from HIP events around the
- * launch on its stream); needs RT_OPT_TIMING. */
+ * launch on its stream — around all of its launches when a deep batch is
+ * split into several); needs RT_OPT_TIMING. */
 int rt_last_kernel_ms(rt_context *ctx, float *ms);
 
 /* RGBA8 unorm packing of a float frame as the shipped GL_RGBA8 surface stores

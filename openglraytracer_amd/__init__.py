@@ -68,6 +68,7 @@ def lib():
             "rt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i),
             "rt_context_set": ([vp, i, i], i),
             "rt_render_batch": ([vp, vp, vp, i, i, i, i, i, i, i, vp, vp], i),
+            "rt_batch_launches": ([vp, vp, i, i], i),
             "rt_render_batch_scenes": ([vp, vp, vp, i, i, i, i, i, i, i, vp, vp], i),
             "rt_render_accumulate": ([vp, vp, vp, i, i, i, i, i, C.c_uint32, i, i, i, vp, vp], i),
             "rt_pack_rgba8": ([vp, C.c_size_t, vp], i),
@@ -343,6 +344,16 @@ def render_batch(ctx, scene, out_ptr, width, height, max_depth, views, block_row
     _check(lib().rt_render_batch(ctx.handle, scene.handle, arr, len(views), width, height, max_depth,
                                  block_rows, n_shards, shard, C.c_void_p(out_ptr),
                                  C.c_void_p(stream) if stream else None))
+
+
+def batch_launches(ctx, scene, n_views, max_depth):
+    """Kernel launches render_batch makes for n_views views of `scene` at
+    max_depth (deep batches split into queued launches of as many views as
+    fit beside the scene in LDS)."""
+    n = lib().rt_batch_launches(ctx.handle, scene.handle, n_views, max_depth)
+    if n < 0:
+        raise RTError(n, lib().rt_last_error().decode())
+    return n
 
 
 def render_batch_scenes(ctx, scenes, out_ptr, width, height, max_depth, views, block_rows=8, n_shards=1,

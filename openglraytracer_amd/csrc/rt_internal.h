@@ -327,4 +327,5 @@ struct rt_scene {
     };
     mutable std::vector<Use> uses;
     mutable bool overflow = false;
+    mutable bool warned = false;  // the overflow's one-time stderr notice was printed
 };

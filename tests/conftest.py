@@ -56,10 +56,11 @@ def gpu_ctx():
 
 
 def dev_zeros(*shape, dtype=None, device="cuda"):
-    """A zero-filled device tensor whose fill has completed: torch queues the
-    fill on its current stream, which nothing orders before a render on the
-    library's own stream (a NULL hipStream_t: the context's non-blocking
-    stream), so an accumulation could otherwise start before the fill."""
+    """A zero-filled device tensor whose fill has completed. Since round 5 a
+    NULL-stream call is ordered after torch's default stream by the library
+    itself (its context stream is a blocking HIP stream, include/rt.h), so
+    this only matters for fills queued on other torch streams; the
+    Monte-Carlo tests use plain torch.zeros on purpose."""
     import torch
     t = torch.zeros(*shape, dtype=dtype, device=device)
     torch.cuda.synchronize()

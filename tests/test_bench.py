@@ -53,6 +53,19 @@ def test_config2_row_tiled_spread_default(n, frames):
     assert v["bit_exact"] and v["frames_checked"] == frames and v["mismatched_pixels"] == 0
     ind = line["independent_frames"]
     assert ind["frames_per_step"] == n * frames and ind["scaling"] == "weak" and ind["value"] > 0
+    check_prediction(line)
+
+
+def check_prediction(line):
+    """N>1 lines judge themselves: DESIGN.md §6's predicted step time (from
+    the committed one-GPU shard timings, at 50 and 100 GB/s per link) beside
+    the measured one, and every rank's collective bytes / collective time."""
+    pred = line["predicted_ms_per_step"]
+    assert pred["measured_ms_per_step"] == line["ms_per_step"]
+    assert pred["ms_per_step_B50"] >= pred["ms_per_step_B100"] > 0
+    assert pred["busiest_link_bytes"] == max(r["link_bytes"] for r in line["timing"]["per_rank"])
+    for r in line["timing"]["per_rank"]:
+        assert r["link_GBps"] > 0 and r["collective_GBps"] >= r["link_GBps"]
 
 
 @pytest.mark.gpu
@@ -71,6 +84,7 @@ def test_config2_two_ranks_row_tiled_gather():
     assert v["bit_exact"] and v["frames_checked"] == 3 and v["mismatched_pixels"] == 0
     ind = line["independent_frames"]
     assert ind["frames_per_step"] == 6 and ind["scaling"] == "weak" and ind["value"] > 0
+    check_prediction(line)
 
 
 @pytest.mark.gpu
@@ -99,12 +113,16 @@ def test_config3_two_ranks_gather():
     # each rank stores its float3 row blocks: half the frame's rows each
     assert line["roofline"]["bytes_per_launch"] == 3840 * 1080 * 12
     assert line["verified"]["bit_exact"] and line["verified"]["frames_checked"] == 1
+    # (no one-GPU shard timings of config 3's row tiles are committed)
+    assert "predicted_ms_per_step" not in line
+    assert all(r["link_GBps"] > 0 for r in line["timing"]["per_rank"])
 
 
 @pytest.mark.gpu
 def test_config5_two_ranks_all_reduce():
     line = run_bench(2, "--workload", "config5", "--steps", "2", "--warmup", "1")
     assert "all_reduce" in line["timing"]["collective"] and line["value"] > 0
+    check_prediction(line)
 
 
 def test_pmc_summary_of_other_sources_is_not_reported(tmp_path, monkeypatch):
@@ -145,6 +163,80 @@ def test_config3_one_gpu_batches_frames():
     cfg = line["config"]
     assert cfg["frames_per_step"] == 7 and cfg["frames_per_launch"] == 7 and cfg["max_depth"] == 2
     assert line["roofline"]["bytes_per_launch"] == 7 * 3840 * 2160 * 16
+    assert line["verified"]["bit_exact"] and line["verified"]["frames_checked"] == [0, 3, 6]
     one = line["single_frame"]
     assert one["frames_per_launch"] == 1 and one["us_per_frame"] > 0 and one["two_streams"]["us_per_frame"] > 0
     assert line["pipelined"]["render_streams"] == 2 and "rgba8_surface" not in line
+
+
+def run_ranks(n, *args, env_extra=None, timeout=180, port=29541):
+    """bench.py --gpus n as n processes of our own (no torchrun, whose agent
+    would terminate the survivors itself): every rank's exit code and stderr."""
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(n), **(env_extra or {}))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n),
+                                       "--dist-backend", "gloo", "--no-cpu-baseline", *args],
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=ROOT))
+    out = []
+    try:
+        for p in procs:
+            _, err = p.communicate(timeout=timeout)
+            out.append((p.returncode, err))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return out
+
+
+def test_a_rank_that_dies_fails_every_rank():
+    """SURVEY.md §5 (an RCCL error aborts the frame): a rank that exits right
+    after joining the group, without a word to its peers, makes the surviving
+    rank's next collective fail; bench.py then ends that rank too, with a
+    message and a nonzero exit, instead of hanging or exiting 0 (gloo on the
+    CPU; no GPU work happens before the startup barrier)."""
+    res = run_ranks(2, "--collective-timeout", "60", env_extra={"RT_BENCH_FAULT": "1:init"})
+    (rc0, err0), (rc1, err1) = res
+    assert rc1 == 3 and "injected fault at init" in err1
+    assert rc0 == 17, (rc0, err0[-2000:])
+    assert "rank 0: step failed, aborting the frame" in err0
+
+
+@pytest.mark.gpu
+def test_a_rank_that_dies_mid_step_fails_every_rank():
+    """The same, with the fault at rank 1's first timed collective (config 2,
+    spread): rank 0 has rendered and packed, its all-to-all fails, and it
+    exits nonzero with a message (two ranks on one GPU, gloo)."""
+    res = run_ranks(2, "--steps", "3", "--warmup", "1", "--frames", "3", "--collective-timeout", "60",
+                    env_extra={"RT_BENCH_FAULT": "1:step"}, port=29542)
+    (rc0, err0), (rc1, err1) = res
+    assert rc1 == 3 and "injected fault at step" in err1
+    assert rc0 == 17, (rc0, err0[-2000:])
+    assert "aborting the frame" in err0
+
+
+@pytest.mark.gpu
+def test_config2_one_gpu_line_checks_itself():
+    """The headline line at N=1: frames 0, 127 and 255 of the last timed step
+    are byte-identical to single renders of the same views; every one-stream
+    figure is the kernel's own (kernel time x launches per step within
+    [0.97, 1.01] of the step time, for the float4 line and for the GL_RGBA8
+    surface); the single-frame rates are medians of 3 repeats."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "12", "--warmup", "3", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    v = line["verified"]
+    assert v["bit_exact"] and v["frames_checked"] == [0, 127, 255] and v["mismatched_pixels"] == 0
+    cfg = line["config"]
+    launches = cfg["frames_per_step"] // cfg["frames_per_launch"]
+    assert launches == 1 and line["timing"]["render_streams"] == 1
+    ratio = line["roofline"]["kernel_ms"] * launches / line["ms_per_step"]
+    assert 0.97 <= ratio <= 1.01, ratio
+    r8 = line["rgba8_surface"]
+    ratio8 = r8["kernel_ms"] * (cfg["frames_per_step"] // r8["frames_per_launch"]) / r8["ms_per_step"]
+    assert 0.97 <= ratio8 <= 1.01, ratio8
+    one = line["single_frame"]
+    assert len(one["repeats_us"]) == 3 and len(one["two_streams"]["repeats_us"]) == 3

@@ -57,7 +57,11 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--workloads", default="config2,config4")
     ap.add_argument("--frames", type=int, default=256, help="config 2: frames per step (bench.py --frames)")
+    ap.add_argument("--out", default=None,
+                    help="also write every record to this JSON file (profiles/shard_timing_latest.json: "
+                         "what bench.py --gpus N predicts its step time from)")
     args = ap.parse_args()
+    records = []
     ns = [int(v) for v in args.ns.split(",")]
     ctx = rt.Context(0)
     ctx.set_timing(False)
@@ -155,8 +159,16 @@ def main():
                     rec["assembly_ms"] = round(timed(lambda: frame.assemble_contiguous(big, F, H, W, 3, idx), 10,
                                                      stream), 5)
             print(json.dumps(rec), flush=True)
+            records.append(rec)
             del buf
         scene.close()
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"tool": "tools/shard_timing.py",
+                       "note": "every rank's per-step work timed on ONE MI355X (the render of each shard, the RGB8 "
+                               "packing, the de-interleave); bench.py --gpus N predicts its step time from these "
+                               "(DESIGN.md §6)",
+                       "build": rt.lib().rt_version().decode(), "records": records}, f, indent=1)
     ctx.close()
 
 
