@@ -112,6 +112,40 @@ constexpr int kGMaskTexels = RT_GMASK_TEXELS;
 constexpr int kGListMax = 15;
 constexpr uint32_t kGListOverflow = 255u;
 static_assert(kGMaskMaxSpheres <= 256, "candidate lists hold sphere slots in bytes");
+// Secondary rays that start on a sphere (round 5; tools/model/
+// origin_list_model.py: 66-73 % of config 4's secondary rays, 58 % of
+// config 3's) look up the spheres they can hit instead of walking the BVH:
+// per sphere s, a cube map of kOListTexels x kOListTexels texels per face
+// (direction_texel's layout) whose texel lists every sphere j that a ray
+// from the ball B(c_s, r_s + 0.001) — every reflection or refraction origin
+// on s (:1010-1023) — with its direction in the texel can hit: the cone of
+// the texel from c_s meets the ball B(c_j, r_j + r_s + 0.001) (the shadow
+// masks' test, float64, with margins), s itself first (a ray inside s
+// leaves through it). The candidates follow in increasing order of a lower
+// bound of their hit distance, |c_j - c_s| - r_j - r_s - margins, so a lane
+// whose closest hit so far (the box's, tested first) lies below the next
+// bound can stop. One 32-B record per (sphere, texel):
+//   byte 0      the number of candidates (255: 255 or more);
+//   bytes 1..25 the first kOListSlots candidates' sphere slots;
+//   bytes 26..31 three uint16 bounds in 1/256 units (rounded down, 65535 at
+//               most): of candidate 8, of candidate 16, and of candidate
+//               kOListSlots (the first one not in the record; 65535 when
+//               there is none). A lane checks the first two before testing
+//               candidates 8 and 16; one that has tested the whole record
+//               and still lies above the third walks the BVH instead.
+// Built for scenes of kOListMinSpheres..kGMaskMaxSpheres spheres, read by the
+// recursive kernels (depth >= 2) through L2, never staged.
+#ifndef RT_OLIST_TEXELS
+#define RT_OLIST_TEXELS 16
+#endif
+constexpr int kOListTexels = RT_OLIST_TEXELS;
+constexpr int kOListSlots = 25;
+constexpr int kOListRecordBytes = 32;
+#ifndef RT_OLIST_FROM
+#define RT_OLIST_FROM 33  // (the wide masks' threshold: smaller scenes keep the BVH walk, their blob unchanged)
+#endif
+constexpr int kOListMinSpheres = RT_OLIST_FROM;
+constexpr float kOListBoundUnit = 1.0f / 256.0f;
 // Sphere BVH node (depth-first order; the left child is the next node):
 // lo = (min xyz, skip) and hi = (max xyz, leaf) where skip is the node after
 // this subtree (-1: end) and leaf = (count << 24) | first sphere slot (0 for
@@ -177,6 +211,7 @@ struct LaunchParams {
     int32_t dmask_bytes;         // bytes per mask: 2, 4 or 8 (at most 16, 32, 64 spheres)
     int32_t off_gmask, gmask_words;  // wide masks in the blob past blob_units (not staged), 16-B units; -1: none
     int32_t off_glist;               // their candidate lists (kGListMax), 16-B units; -1: none
+    int32_t off_olist;               // secondary rays' origin-sphere candidate lists (kOListSlots), 16-B units; -1: none
     int32_t blob_units;      // blob size, 16-B units
     // Monte-Carlo accumulation (render_kernel<D, true>): samples
     // [sample0, sample0 + spp) per pixel, jittered inside the pixel when
@@ -224,6 +259,7 @@ struct DeviceScene {
     int32_t off_bvh = 0, n_bvh = 0, off_blink = 0, off_cone = 0;
     int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
     int32_t off_gmask = -1, gmask_words = 0, off_glist = -1;
+    int32_t off_olist = -1;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
 };
 

@@ -360,6 +360,9 @@ struct Scene {
     const uint64_t *gmask;  // wide masks in global memory: [live light][texel][word] (nullptr: none)
     const uint4 *glist;     // their candidate lists: [live light][texel] (nullptr: none)
     int gwords;
+    // secondary rays' origin-sphere candidate lists, 32-B records
+    // [sphere][texel] (rt_internal.h kOListSlots; nullptr: none)
+    const uint4 *olist;
     // The same box and light records in the device blob through the constant
     // address space: a wave-uniform record index becomes scalar loads into
     // SGPRs (no LDS round trip, no VGPRs) — used where the index is uniform.
@@ -617,9 +620,13 @@ __device__ __forceinline__ bool node_hit(const RayInv &q, float4 lo, float4 hi, 
     return tn <= tf && tf >= 0.0f && tn <= t_limit;
 }
 
-// get_closest_collision (:738-782). Called with all lanes active.
+// direction_texel, defined below
+__device__ __forceinline__ int direction_texel(int n, v3 u);
+
+// get_closest_collision (:738-782). Called with all lanes active. origin:
+// the sphere slot a secondary ray starts on (-1: the camera or a box).
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool valid) {
+__device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool valid, int origin) {
     Hit h{10000.0f, -1, 0, 0};
     RT_STAT(kPrimary ? 0 : 1, valid);
     RT_STAT(kPrimary ? 13 : 2, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
@@ -663,13 +670,57 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
             }
         }
     } else if (!kPrimary && S.cull && S.nbvh > 0) {
+        bool walk = valid;  // lanes that walk the BVH below
+        if (S.olist) {
+            // A ray that starts on sphere `origin` tests the candidates of its
+            // direction's texel in that sphere's list (rt_internal.h
+            // kOListSlots: every sphere it can hit, its own first, then by a
+            // lower bound of the hit distance) instead of walking the BVH; it
+            // stops once its closest hit lies below the next stored bound. A
+            // lane whose list goes on past the record (and whose hit lies
+            // above the next bound), or without an origin sphere or a usable
+            // direction, walks the BVH. The candidates are a superset of the
+            // spheres the ray can hit and the closest hit is order-independent
+            // (explicit index tie-break): the result is the walk's, bit for
+            // bit. CPU model (tools/model/origin_list_model.py, config 4):
+            // 30.3 BVH node iterations + sphere passes per wave call become
+            // 4.9 list passes + 7.1 for the lanes left to the BVH.
+            const int tex = (valid && origin >= 0) ? direction_texel(kOListTexels, r.dir) : -1;
+            uint4 ra = make_uint4(0u, 0u, 0u, 0u), rb = ra;
+            if (tex >= 0) {
+                const uint4 *rec =
+                    S.olist + 2 * (static_cast<size_t>(origin) * (6 * kOListTexels * kOListTexels) + tex);
+                ra = rec[0];
+                rb = rec[1];
+            }
+            const uint32_t cnt = ra.x & 0xFFu;
+            uint32_t n = cnt < static_cast<uint32_t>(kOListSlots) ? cnt : static_cast<uint32_t>(kOListSlots);
+#pragma unroll
+            for (int i = 0; i < kOListSlots; ++i) {  // i: a constant after unrolling (byte i + 1 of the record)
+                if (!__any(static_cast<uint32_t>(i) < n)) break;
+                RT_STAT(14, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
+                if (i == 8 || i == 16) {  // the stored bounds of candidates 8 and 16
+                    const uint32_t q = i == 8 ? (rb.z >> 16) : (rb.w & 0xFFFFu);
+                    if (h.t < static_cast<float>(q) * kOListBoundUnit) n = 0;
+                }
+                if (static_cast<uint32_t>(i) < n) {
+                    RT_STAT(15, true);
+                    const uint32_t word = (i + 1) < 4 ? ra.x : (i + 1) < 8 ? ra.y : (i + 1) < 12 ? ra.z
+                                        : (i + 1) < 16 ? ra.w : (i + 1) < 20 ? rb.x : (i + 1) < 24 ? rb.y : rb.z;
+                    const int sl = static_cast<int>((word >> (8 * ((i + 1) & 3))) & 0xFFu);
+                    test_sphere(S, sl, r.start, d2, qa2, qa4, floor, false, h);
+                }
+            }
+            const float bend = static_cast<float>(rb.w >> 16) * kOListBoundUnit;
+            walk = valid && (tex < 0 || (cnt > static_cast<uint32_t>(kOListSlots) && !(h.t < bend)));
+        }
         // secondary rays: stackless depth-first BVH walk (skip links)
         // (testing first the sphere a secondary ray starts inside — a
         // refraction into or a reflection inside a sphere — changed no node
         // test: the ordered walk reaches its leaf first anyway; config 4
         // +1.3 %, config 3 +1.6 %, r03c)
         const RayInv q = ray_inv(r);
-        int node = valid ? 0 : -1;
+        int node = walk ? 0 : -1;
         // while-while: each lane walks nodes until it holds a leaf (or its
         // walk ends); then the wave tests the spheres of every held leaf
         // together, so the sphere tests of lanes that reach leaves on
@@ -712,9 +763,9 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
     return h;
 }
 template <bool kPrimary>
-__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid) {
+__device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid, int origin = -1) {
     RT_CYC(kPrimary ? kCycClosest1 : kCycClosest2);
-    const Hit h = closest_impl<kPrimary>(S, r, valid);
+    const Hit h = closest_impl<kPrimary>(S, r, valid, origin);
     RT_CYC_AFTER(kCycWalk, h.t);
     return h;
 }
@@ -1235,6 +1286,7 @@ struct Frame {
     v3 col;       // phong, then mix(phong, R, rho) once the reflection returned
     v3 rs, rd;    // pending refraction ray (:1010-1023)
     int flags;    // 1: refraction spawned; 2: waiting for the reflection; 4: for the refraction;
+                  // | (the hit sphere's slot + 1) << 11 (the refraction child's origin sphere)
                   // | material << 3 (rho and tau read back from it: a 40-B frame instead of
                   // 48, config 4 18.68 -> 18.26 ms, config 3 1.022 -> 1.000 ms; the flags
                   // beside the colour, so a pop reads one 16-B word, measured even, r03h)
@@ -1292,11 +1344,13 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
     int level = 0;
     bool done = !active;
     bool first = true;
+    int origin = -1;  // the sphere slot the lane's ray starts on (-1: the camera or a box)
     while (__any(!done)) {
         RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
         const bool valid = !done;
         const bool primary = first;
-        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid);
+        // (origin lists: depth >= 2 only, S.olist)
+        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid, kDepth >= 2 ? origin : -1);
         first = false;
         const bool hit = valid && h.obj >= 0;
         const Collision c = primary ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
@@ -1321,8 +1375,12 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
                 const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
                 fr.rd = refract(ray.dir, c.n, ratio);
             }
-            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3);
+            // (with the sphere its children start on, + 1, from bit 11: the
+            // refraction child's origin when the walk comes back to it)
+            const int here = h.slot >= 0 ? h.slot : -1;
+            fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3) | (kDepth >= 2 ? (here + 1) << 11 : 0);
             F.set(level, fr);
+            if constexpr (kDepth >= 2) origin = here;
             if (sr) {
                 ray.start = add(c.p, muls(c.n, 0.001f));
                 ray.dir = reflect(ray.dir, c.n);
@@ -1338,7 +1396,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
         bool next_child = false;
         while (level > 0 && !next_child) {
             Frame fr = F.get(level - 1);
-            const MatRec &fm = S.mat[fr.flags >> 3];
+            const MatRec &fm = S.mat[(fr.flags >> 3) & 0xFF];
             const float rho = fm.reflectivity, tau = fm.transparency;
             if (fr.flags & 2) {
                 fr.col = mix(fr.col, value, rho);
@@ -1347,6 +1405,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
                     F.set(level - 1, fr);
                     ray.start = fr.rs;
                     ray.dir = fr.rd;
+                    if constexpr (kDepth >= 2) origin = (fr.flags >> 11) - 1;
                     next_child = true;
                 } else {
                     value = fr.col;
@@ -1763,6 +1822,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.gmask = kDepth >= 2 && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;
     S.gwords = p.gmask_words;
     S.glist = S.gmask && p.off_glist >= 0 ? reinterpret_cast<const uint4 *>(blob + p.off_glist) : nullptr;
+    S.olist = kDepth >= 2 && p.off_olist >= 0 ? reinterpret_cast<const uint4 *>(blob + p.off_olist) : nullptr;
     S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
     S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
     S.nbvh = p.n_bvh;

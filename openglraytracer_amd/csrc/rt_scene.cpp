@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "rt_internal.h"
@@ -652,7 +653,10 @@ struct MaskCones {
         double w[3], reach, cr, sr;  // centre direction, reach and its cos / sin
     };
     std::vector<Block> blocks;
+    // per block, its kMaskSubBlock x kMaskSubBlock sub-blocks (same reach rule)
+    std::vector<std::vector<Block>> subs;
 };
+constexpr int kMaskSubBlock = 2;
 
 const MaskCones &mask_cones(int n) {
     static std::mutex mu;
@@ -704,24 +708,32 @@ const MaskCones &mask_cones(int n) {
                 mc->ca[t] = std::cos(alpha[t]);
                 mc->sa[t] = std::sin(alpha[t]);
             }
+        auto block = [&](int r0, int c0, int size) {
+            MaskCones::Block bl;
+            bl.face = f;
+            bl.r0 = r0;
+            bl.c0 = c0;
+            bl.r1 = std::min(n, r0 + size);
+            bl.c1 = std::min(n, c0 + size);
+            bl.reach = cone(-1.0 + 2.0 * bl.c0 / n, -1.0 + 2.0 * bl.c1 / n, -1.0 + 2.0 * bl.r0 / n,
+                            -1.0 + 2.0 * bl.r1 / n, bl.w);
+            double amax = 0.0;
+            for (int row = bl.r0; row < bl.r1; ++row)
+                for (int col = bl.c0; col < bl.c1; ++col)
+                    amax = std::max(amax, alpha[(static_cast<size_t>(f) * n + row) * n + col]);
+            bl.reach += amax;
+            bl.cr = std::cos(bl.reach);
+            bl.sr = std::sin(bl.reach);
+            return bl;
+        };
         for (int r0 = 0; r0 < n; r0 += kMaskBlock)
             for (int c0 = 0; c0 < n; c0 += kMaskBlock) {
-                MaskCones::Block bl;
-                bl.face = f;
-                bl.r0 = r0;
-                bl.c0 = c0;
-                bl.r1 = std::min(n, r0 + kMaskBlock);
-                bl.c1 = std::min(n, c0 + kMaskBlock);
-                bl.reach = cone(-1.0 + 2.0 * bl.c0 / n, -1.0 + 2.0 * bl.c1 / n, -1.0 + 2.0 * bl.r0 / n,
-                                -1.0 + 2.0 * bl.r1 / n, bl.w);
-                double amax = 0.0;
-                for (int row = bl.r0; row < bl.r1; ++row)
-                    for (int col = bl.c0; col < bl.c1; ++col)
-                        amax = std::max(amax, alpha[(static_cast<size_t>(f) * n + row) * n + col]);
-                bl.reach += amax;
-                bl.cr = std::cos(bl.reach);
-                bl.sr = std::sin(bl.reach);
-                mc->blocks.push_back(bl);
+                mc->blocks.push_back(block(r0, c0, kMaskBlock));
+                const MaskCones::Block &bl = mc->blocks.back();
+                std::vector<MaskCones::Block> sub;
+                for (int r = bl.r0; r < bl.r1; r += kMaskSubBlock)
+                    for (int c = bl.c0; c < bl.c1; c += kMaskSubBlock) sub.push_back(block(r, c, kMaskSubBlock));
+                mc->subs.push_back(std::move(sub));
             }
     }
     slot = std::move(mc);
@@ -794,6 +806,173 @@ static void build_direction_masks(const std::vector<SphereRec> &sph, const std::
                     }
             }
     }
+}
+
+// Origin-sphere candidate lists of the secondary rays (rt_internal.h,
+// kOListSlots): float64 geometry, the spheres in their final (BVH) slot order.
+// Every reflection or refraction ray that leaves sphere s starts within
+// 0.001 of its surface (:1010-1023: p +- 0.001 n), so inside the ball
+// B(c_s, r_s + 0.001); it can hit sphere j only in a direction within
+// asin(rin / d) of (c_j - c_s) / d, rin = r_j + r_s + 0.001 + margins, d =
+// |c_j - c_s| (any direction when d <= rin) — the shadow masks' cone test
+// with the origin ball folded into the target, texel by texel in the blocks
+// the sphere's cone reaches. The margins (1e-3 + 1e-4 of the coordinates'
+// magnitude, plus 1e-3 rad) dwarf the float32 error of the kernel's hit
+// points, offsets and approximate texel lookup. A candidate's bound is a
+// lower bound of the ray parameter of any hit on it from that ball: the
+// distance between the balls, shrunk by the same margins and by 1e-5 for
+// ray directions that are unit vectors only up to rounding; stored rounded
+// down in 1/256 units, so a lane that stops on `best t < bound` drops only
+// spheres whose hit would lie strictly farther (no tie can be lost).
+static void origin_lists_range(const std::vector<SphereRec> &sph, const std::vector<SphereMeta> &smeta, int n,
+                               std::vector<uint8_t> &out, size_t s_begin, size_t s_end) {
+    const size_t ns = sph.size();
+    const MaskCones &mc = mask_cones(n);
+    const size_t texels = static_cast<size_t>(6) * n * n;
+    std::vector<double> ax(3 * ns), ch(ns), sh(ns), lb(ns), reach(ns);
+    std::vector<char> every(ns);
+    // the spheres' cone data in list order (o*), a block's candidates (k*) and
+    // a sub-block's (s*), contiguous
+    std::vector<int> order(ns), kq(ns), sq(ns);
+    std::vector<double> ox(ns), oy(ns), oz(ns), oc(ns), osn(ns), orc(ns);
+    std::vector<double> kx(ns), ky(ns), kz(ns), kc(ns), ksn(ns), kr(ns);
+    std::vector<double> sx(ns), sy(ns), sz(ns), sc(ns), ss(ns);
+    std::vector<char> oe(ns), ke(ns), se(ns), keep(ns), hit(ns);
+    std::vector<std::pair<double, int>> list;  // one texel's candidates: (bound, slot)
+    auto quant = [](double x) -> uint16_t {  // rounded down, saturating (a smaller bound stays a bound)
+        if (!(x > 0.0)) return 0;
+        const double q = std::floor(x / static_cast<double>(kOListBoundUnit));
+        return static_cast<uint16_t>(std::min(q, 65535.0));
+    };
+    for (size_t s = s_begin; s < s_end; ++s) {
+        const double cs[3] = {sph[s].cx, sph[s].cy, sph[s].cz};
+        const double rs = smeta[s].radius;
+        const double ms = std::sqrt(cs[0] * cs[0] + cs[1] * cs[1] + cs[2] * cs[2]);
+        for (size_t j = 0; j < ns; ++j) {
+            const double v[3] = {double(sph[j].cx) - cs[0], double(sph[j].cy) - cs[1], double(sph[j].cz) - cs[2]};
+            const double d = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+            const double cj = std::sqrt(double(sph[j].cx) * sph[j].cx + double(sph[j].cy) * sph[j].cy +
+                                        double(sph[j].cz) * sph[j].cz);
+            const double rj = smeta[j].radius;
+            const double margin = 1e-3 + 1e-4 * (d + ms + cj + rs + rj);
+            const double rin = rj + rs + 0.001 + margin;
+            const bool ok = std::isfinite(d) && std::isfinite(rin) && std::isfinite(margin);
+            lb[j] = j == s ? -1.0 : (ok ? std::max(0.0, (d - rj - rs - 0.001 - 2.0 * margin) * (1.0 - 1e-5)) : 0.0);
+            every[j] = !ok || d <= rin;
+            if (every[j]) continue;
+            for (int k = 0; k < 3; ++k) ax[3 * j + k] = v[k] / d;
+            const double half = std::asin(std::min(1.0, rin / d));
+            reach[j] = half + 1e-3;
+            ch[j] = std::cos(reach[j]);
+            sh[j] = std::sin(reach[j]);
+        }
+        // The spheres in list order, (bound, slot) ascending: every list
+        // below is built by walking them in this order, so it comes out
+        // sorted. A (sub-)block is skipped for sphere j when j's cone misses
+        // the block's reach (every texel the texel test accepts lies in an
+        // accepted block and sub-block); the tests run over contiguous
+        // arrays of the candidates' cone data.
+        for (size_t j = 0; j < ns; ++j) order[j] = static_cast<int>(j);
+        std::sort(order.begin(), order.end(), [&](int x, int y) { return lb[x] < lb[y] || (lb[x] == lb[y] && x < y); });
+        for (size_t q = 0; q < ns; ++q) {
+            const int j = order[q];
+            ox[q] = ax[3 * j];
+            oy[q] = ax[3 * j + 1];
+            oz[q] = ax[3 * j + 2];
+            oc[q] = ch[j];
+            osn[q] = sh[j];
+            orc[q] = reach[j];
+            oe[q] = every[j];
+        }
+        // reach test of a block against candidates [0, m) of (x, y, z, c, sn, r, e): keep[] = 1 if it may reach
+        auto reach_test = [](const MaskCones::Block &bl, size_t m, const double *x, const double *y, const double *z,
+                             const double *c, const double *sn, const double *r, const char *e, char *keep) {
+            for (size_t q = 0; q < m; ++q)
+                keep[q] = e[q] | static_cast<char>(bl.reach + r[q] >= 3.141592653589793) |
+                          static_cast<char>(bl.w[0] * x[q] + bl.w[1] * y[q] + bl.w[2] * z[q] >=
+                                            bl.cr * c[q] - bl.sr * sn[q] - 1e-9);
+        };
+        for (size_t k = 0; k < mc.blocks.size(); ++k) {
+            reach_test(mc.blocks[k], ns, ox.data(), oy.data(), oz.data(), oc.data(), osn.data(), orc.data(), oe.data(),
+                       keep.data());
+            size_t mk = 0;  // the block's candidates, in list order
+            for (size_t q = 0; q < ns; ++q)
+                if (keep[q]) {
+                    kq[mk] = static_cast<int>(q);
+                    kx[mk] = ox[q];
+                    ky[mk] = oy[q];
+                    kz[mk] = oz[q];
+                    kc[mk] = oc[q];
+                    ksn[mk] = osn[q];
+                    kr[mk] = orc[q];
+                    ke[mk] = oe[q];
+                    ++mk;
+                }
+            for (const MaskCones::Block &sb : mc.subs[k]) {
+                reach_test(sb, mk, kx.data(), ky.data(), kz.data(), kc.data(), ksn.data(), kr.data(), ke.data(),
+                           keep.data());
+                size_t m = 0;  // the sub-block's candidates, in list order
+                for (size_t q = 0; q < mk; ++q)
+                    if (keep[q]) {
+                        sq[m] = kq[q];
+                        sx[m] = kx[q];
+                        sy[m] = ky[q];
+                        sz[m] = kz[q];
+                        sc[m] = kc[q];
+                        ss[m] = ksn[q];
+                        se[m] = ke[q];
+                        ++m;
+                    }
+                for (int row = sb.r0; row < sb.r1; ++row)
+                    for (int col = sb.c0; col < sb.c1; ++col) {
+                        const size_t t = (static_cast<size_t>(sb.face) * n + row) * n + col;
+                        const double w0 = mc.w[3 * t], w1 = mc.w[3 * t + 1], w2 = mc.w[3 * t + 2];
+                        const double ca = mc.ca[t], sa = mc.sa[t];
+                        // (reach < pi / 2 + 1e-3 and a texel's half-angle is small: the summed
+                        // angle stays below pi, where the cosine test is exact)
+                        for (size_t q = 0; q < m; ++q)
+                            hit[q] = se[q] | static_cast<char>(w0 * sx[q] + w1 * sy[q] + w2 * sz[q] >=
+                                                               ca * sc[q] - sa * ss[q] - 1e-12);
+                        list.clear();  // (list order already)
+                        for (size_t q = 0; q < m; ++q)
+                            if (hit[q]) list.push_back({lb[order[sq[q]]], order[sq[q]]});
+                        uint8_t *rec = out.data() + (s * texels + t) * kOListRecordBytes;
+                        const size_t cnt = list.size();
+                        rec[0] = static_cast<uint8_t>(std::min<size_t>(cnt, 255));
+                        for (size_t i = 0; i < cnt && i < static_cast<size_t>(kOListSlots); ++i)
+                            rec[1 + i] = static_cast<uint8_t>(list[i].second);
+                        const uint16_t bnd[3] = {cnt > 8 ? quant(list[8].first) : uint16_t{65535},
+                                                 cnt > 16 ? quant(list[16].first) : uint16_t{65535},
+                                                 cnt > static_cast<size_t>(kOListSlots)
+                                                     ? quant(list[kOListSlots].first)
+                                                     : uint16_t{65535}};
+                        std::memcpy(rec + 1 + kOListSlots, bnd, sizeof bnd);
+                    }
+            }
+        }
+    }
+}
+
+// The lists of all spheres: independent per origin sphere, built on up to 16
+// host threads (256 spheres: about 130 ms of host work on one thread).
+static void build_origin_lists(const std::vector<SphereRec> &sph, const std::vector<SphereMeta> &smeta, int n,
+                               std::vector<uint8_t> &out) {
+    const size_t ns = sph.size();
+    out.assign(ns * static_cast<size_t>(6) * n * n * kOListRecordBytes, 0);
+    (void)mask_cones(n);  // (built once, before the workers share it)
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t n_thr = std::min<size_t>({16, hw, (ns + 15) / 16});
+    if (n_thr <= 1) {
+        origin_lists_range(sph, smeta, n, out, 0, ns);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const size_t per = (ns + n_thr - 1) / n_thr;
+    for (size_t k = 0; k < n_thr; ++k) {
+        const size_t a = k * per, b = std::min(ns, a + per);
+        if (a < b) pool.emplace_back(origin_lists_range, std::cref(sph), std::cref(smeta), n, std::ref(out), a, b);
+    }
+    for (std::thread &t : pool) t.join();
 }
 
 int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
@@ -1070,6 +1249,15 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         ds.off_glist = off;
         off += units(glist.size());
     }
+    // The secondary rays' origin-sphere candidate lists (rt_internal.h
+    // kOListSlots), past the staged part like the wide masks.
+    std::vector<uint8_t> olist;
+    ds.off_olist = -1;
+    if (sph.size() >= static_cast<size_t>(kOListMinSpheres) && sph.size() <= 256) {
+        build_origin_lists(sph, smeta, kOListTexels, olist);
+        ds.off_olist = off;
+        off += units(olist.size());
+    }
     ds.n_spheres = static_cast<int32_t>(sph.size());
     ds.n_boxes = static_cast<int32_t>(boxes.size());
     ds.n_mats = n_mats;
@@ -1090,6 +1278,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     if (ds.off_dmask >= 0) put(ds.off_dmask, dmask_bytes.data(), dmask_bytes.size());
     if (ds.off_gmask >= 0) put(ds.off_gmask, gmask.data(), gmask.size() * 8);
     if (ds.off_glist >= 0) put(ds.off_glist, glist.data(), glist.size());
+    if (ds.off_olist >= 0) put(ds.off_olist, olist.data(), olist.size());
     return RT_OK;
 }
 

@@ -372,3 +372,105 @@ def test_camera_short_division_ranges_hold_on_real_frames(t):
                 assert (np.abs(nz) >= 2.0 ** -60).all() and (np.abs(nz) <= 2.0 ** 60).all()
             wv = np.abs(comp[3])
             assert (wv >= 2.0 ** -20).all() and (wv <= 2.0 ** 20).all()
+
+
+def _scene_blob(objs):
+    """The blob rt_scene_create would upload (rt_debug_scene_blob) and its
+    layout meta (DeviceScene offsets in 16-B units and counts)."""
+    import ctypes as C
+    L = rt.lib()
+    f = L.rt_debug_scene_blob
+    f.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_longlong,
+                  C.c_void_p]
+    mats, lights = rt.reference_materials(), rt.reference_lights()
+    oa = (rt.Object * len(objs))(*objs)
+    ma = (rt.Material * len(mats))(*mats)
+    la = (rt.Light * len(lights))(*lights)
+    meta = np.zeros(24, np.int32)
+    n = f(oa, len(objs), ma, len(mats), la, len(lights), None, 0, meta.ctypes.data)
+    assert n > 0
+    buf = np.zeros(n, np.uint8)
+    f(oa, len(objs), ma, len(mats), la, len(lights), buf.ctypes.data, n, meta.ctypes.data)
+    return buf, meta
+
+
+def _direction_texel(n, u):
+    """rt_kernel.hip direction_texel in float32 (the approximate reciprocal
+    replaced by a division: the lists' margins cover either)."""
+    u = np.asarray(u, np.float32)
+    ax_, ay, az = np.abs(u)
+    fx = ax_ >= ay and ax_ >= az
+    fy = (not fx) and ay >= az
+    um = u[0] if fx else (u[1] if fy else u[2])
+    ua = u[1] if fx else u[0]
+    ub = u[2] if (fy or fx) else u[1]
+    face = 2 * (0 if fx else (1 if fy else 2)) + (1 if um < 0 else 0)
+    am = abs(um)
+    if not (1e-20 < am < 1e30):
+        return -1
+    h = np.float32(0.5 * n) / np.float32(am)
+    col = min(max(int(np.floor(ua * h + np.float32(0.5 * n))), 0), n - 1)
+    row = min(max(int(np.floor(ub * h + np.float32(0.5 * n))), 0), n - 1)
+    return (face * n + row) * n + col
+
+
+@pytest.mark.parametrize("n_spheres,seed", [(256, 0), (64, 0), (40, 3)])
+def test_origin_lists_hold_every_hit_and_their_bounds_hold(n_spheres, seed):
+    """The secondary rays' origin-sphere candidate lists (rt_internal.h
+    kOListSlots) on the CPU: for rays leaving random points of random
+    spheres (p +- 0.001 n, reflection and refraction origins, :1010-1023) in
+    random directions, the sphere the ray hits first (float64) is in its
+    texel's list; a lane walking the record as the kernel does (stop when the
+    closest hit so far lies below the stored bound of candidate 8 or 16;
+    fall back to the BVH past the record unless below the record-end bound)
+    never stops before the true closest hit; and the record is sorted with
+    the origin sphere first."""
+    objs = rt.bench_objects(n_spheres, seed)
+    buf, meta = _scene_blob(objs)
+    off_sph, off_smeta, ns, off_olist = int(meta[1]), int(meta[2]), int(meta[17]), int(meta[21])
+    assert ns == n_spheres and off_olist > 0
+    f4 = buf.view(np.float32).reshape(-1, 4)
+    sph = f4[off_sph:off_sph + ns].astype(np.float64)
+    rad = f4[off_smeta:off_smeta + ns, 2].astype(np.float64)
+    n_tex = 6 * 16 * 16
+    rec = buf[off_olist * 16: off_olist * 16 + ns * n_tex * 32].reshape(ns, n_tex, 32)
+    assert (rec[:, :, 1] == np.arange(ns)[:, None]).all()  # own sphere first
+    unit = 1.0 / 256.0
+    rng = np.random.default_rng(seed + 11)
+    checked = stops = 0
+    for _ in range(3000):
+        s = int(rng.integers(ns))
+        nrm = rng.normal(size=3)
+        nrm /= np.linalg.norm(nrm)
+        p = sph[s, :3] + rad[s] * nrm + (0.001 if rng.random() < 0.7 else -0.001) * nrm
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        oc = p[None, :] - sph[:, :3]
+        b = oc @ d
+        qc = np.einsum("ij,ij->i", oc, oc) - rad ** 2
+        disc = b * b - qc
+        sq = np.sqrt(np.maximum(disc, 0))
+        t1, t2 = -b - sq, -b + sq
+        t = np.where(disc >= 0, np.where(t1 > 0, t1, np.where(t2 > 0, t2, np.inf)), np.inf)
+        tex = _direction_texel(16, d)
+        assert tex >= 0
+        r = rec[s, tex]
+        cnt = int(r[0])
+        slots = list(r[1:1 + min(cnt, 25)])
+        b8, b16, bend = (int(v) * unit for v in r[26:32].view(np.uint16))
+        hit = int(np.argmin(t)) if np.isfinite(t).any() else -1
+        if hit >= 0 and t[hit] > 1e-6:
+            checked += 1
+            tbox = 2.0 + 18.0 * rng.random()  # the room's exit: the walk starts from the box's t
+            best = tbox
+            tested = []
+            for i, sl in enumerate(slots):
+                if (i == 8 and best < b8) or (i == 16 and best < b16):
+                    stops += 1
+                    break
+                tested.append(sl)
+                best = min(best, t[sl])
+            fallback = cnt > 25 and not (best < bend)
+            if t[hit] < tbox and not fallback:
+                assert hit in tested, (s, tex, hit, slots, t[hit])
+    assert checked > 2000 and (stops > 0 or n_spheres < 64)

@@ -55,6 +55,21 @@ def load(spec):
 
 
 libs = {b: load(b) for b in builds}
+# the register / spill gate (tools/resources.py): every build's registers and
+# scratch head the log; a variant whose scratch grows (or occupancy drops) at
+# any render kernel against the first build is not timed unless
+# AB_ALLOW_SPILL=1 says its prediction accounts for it
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import resources  # noqa: E402
+for b in builds:
+    print(resources.report(b.split(":")[0])[1], flush=True)
+for b in builds[1:]:
+    bad = resources.gate(builds[0].split(":")[0], b.split(":")[0])
+    for k, x, y in bad:
+        print("# GATE %s vs %s, %s: scratch %d -> %d B/lane, %d -> %d waves/SIMD" % (
+            b, builds[0], k, x["scratch"], y["scratch"], x["waves_per_simd"], y["waves_per_simd"]), flush=True)
+    if bad and os.environ.get("AB_ALLOW_SPILL") != "1":
+        sys.exit("register gate: %s spills more than %s (AB_ALLOW_SPILL=1 to time it anyway)" % (b, builds[0]))
 stream = torch.cuda.Stream()
 torch.cuda.set_stream(stream)
 mats = rt.reference_materials()

@@ -126,6 +126,7 @@ def trace(S, o, d):
     nrm = np.where(use_box[:, None], nb, ns)
     inside = np.where(use_box, tn < 0, inside_s)
     mat = np.where(use_box, S["bmat"], S["mat"][k])
+    trace.obj = np.where(hit, np.where(use_box, -1, k), -2)  # hit object: -1 the box, >= 0 a sphere, -2 none
     return hit, p, nrm, inside, mat
 
 
@@ -136,18 +137,26 @@ def refract(i, n, eta):
     return np.where((kk < 0)[:, None], 0.0, r)
 
 
-def build_trees(S, w, h, depth, tiles, rng):
+def build_trees(S, w, h, depth, tiles, rng, adjacent=1):
     """Every pixel's ray tree, level by level. Returns per-node arrays:
-    pixel, level, hit, spawned reflection / refraction child node ids."""
+    pixel, level, hit, spawned reflection / refraction child node ids.
+    adjacent > 1: the tiles come in runs of that many horizontally adjacent
+    wave tiles (the four waves of a queued work-group start on adjacent tiles)."""
     wtx, wty = w // 8, h // 8
-    pick = rng.choice(wtx * wty, size=tiles, replace=False)
+    if adjacent > 1:
+        runs = rng.choice(wtx // adjacent * wty, size=tiles // adjacent, replace=False)
+        start = (runs // (wtx // adjacent)) * wtx + (runs % (wtx // adjacent)) * adjacent
+        pick = (start[:, None] + np.arange(adjacent)[None, :]).reshape(-1)
+    else:
+        pick = rng.choice(wtx * wty, size=tiles, replace=False)
     lane = np.arange(64)
     xs = ((pick % wtx)[:, None] * 8 + lane % 8).reshape(-1).astype(np.float64)
     ys = ((pick // wtx)[:, None] * 8 + lane // 8).reshape(-1).astype(np.float64)
     o, d = camera_rays(w, h, xs, ys)
     n_pix = len(xs)
-    pix, lev, hitl, cr, ct, ro, rd = [], [], [], [], [], [], []
-    cur = dict(o=o, d=d, pix=np.arange(n_pix), parent=-np.ones(n_pix, int), kind=np.zeros(n_pix, int))
+    pix, lev, hitl, cr, ct, ro, rd, src = [], [], [], [], [], [], [], []
+    cur = dict(o=o, d=d, pix=np.arange(n_pix), parent=-np.ones(n_pix, int), kind=np.zeros(n_pix, int),
+               src=np.full(n_pix, -3))
     base = 0
     for level in range(depth + 1):
         m = len(cur["o"])
@@ -156,6 +165,7 @@ def build_trees(S, w, h, depth, tiles, rng):
         hit, p, nrm, inside, mat = trace(S, cur["o"], cur["d"])
         ids = base + np.arange(m)
         pix.append(cur["pix"])
+        src.append(cur["src"])
         ro.append(cur["o"])
         rd.append(cur["d"])
         lev.append(np.full(m, level))
@@ -179,14 +189,17 @@ def build_trees(S, w, h, depth, tiles, rng):
         dtr = refract(cur["d"], nrm, eta)
         o2 = np.concatenate([(p + 0.001 * nrm)[sr], (p - 0.001 * nrm)[st]])
         d2 = np.concatenate([dref[sr], dtr[st]])
+        obj = trace.obj
         cur = dict(o=o2, d=d2, pix=np.concatenate([cur["pix"][sr], cur["pix"][st]]),
                    parent=np.concatenate([ids[sr], ids[st]]),
-                   kind=np.concatenate([np.zeros(sr.sum(), int), np.ones(st.sum(), int)]))
+                   kind=np.concatenate([np.zeros(sr.sum(), int), np.ones(st.sum(), int)]),
+                   src=np.concatenate([obj[sr], obj[st]]))
     pix, lev, hitl = np.concatenate(pix), np.concatenate(lev), np.concatenate(hitl)
     cr, ct = np.concatenate(cr), np.concatenate(ct)
     for kind, par, child in links:
         (cr if kind == 0 else ct)[par] = child
     build_trees.rays = (np.concatenate(ro), np.concatenate(rd))
+    build_trees.src = np.concatenate(src)  # the object a ray starts on (-3: camera ray, -1: the box, >= 0: sphere)
     return n_pix, pix, lev, hitl, cr, ct
 
 
