@@ -319,6 +319,11 @@ int rt_multi_last_ms(rt_multi *m, float *kernel_ms, float *gather_ms, float *ass
  * 16 spheres + 1 box);
  * 0: every work-group derives them on the device. Output is identical. */
 #define RT_OPT_FRAME_CONSTS 4
+/* RT_OPT_ORIGIN_LISTS (default 1): a secondary ray that starts on a sphere
+ * of a scene of 33-256 spheres tests the candidates its direction selects in
+ * that sphere's precomputed list instead of walking the sphere BVH
+ * (depth >= 2); 0: every secondary ray walks the BVH. Output is identical. */
+#define RT_OPT_ORIGIN_LISTS 7
 /* (option 6, a tolerance tier that summed the recursion's colours forward
  * instead of mixing them on the way back up, measured even with the exact
  * walk and was removed: DESIGN.md §3.) */

@@ -223,6 +223,11 @@ class Context:
         (default), else derived by every work-group (output identical)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_FRAME_CONSTS, 1 if on else 0))
 
+    def set_origin_lists(self, on):
+        """RT_OPT_ORIGIN_LISTS: secondary rays leaving a sphere test its
+        precomputed candidate list instead of walking the BVH (output identical)."""
+        _check(lib().rt_context_set(self._h, abi.RT_OPT_ORIGIN_LISTS, 1 if on else 0))
+
     def set_output(self, fmt):
         """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel),
         abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)

@@ -327,6 +327,7 @@ struct rt_context {
     int timing = 1;   // RT_OPT_TIMING
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int host_consts = 1;  // RT_OPT_FRAME_CONSTS
+    int origin_lists = 1;  // RT_OPT_ORIGIN_LISTS
     // device-side view batches (> kMaxViews views): per slot a device buffer,
     // its pinned host staging and an event after the last launch that read it
     void *batch_dev[rtamd::kBatchSlots] = {};

@@ -470,6 +470,31 @@ def test_culling_and_bvh_change_nothing(gpu_ctx, cfg, w, h):
     assert np.array_equal(on, o), parity_stats(on, o)
 
 
+@pytest.mark.parametrize("n_spheres,seed,depth,w,h", [(256, 0, 4, 320, 180), (64, 0, 2, 480, 270),
+                                                       (64, 0, 5, 320, 180), (40, 7, 3, 256, 144),
+                                                       (150, 3, 4, 320, 180), (33, 9, 9, 160, 90)])
+def test_origin_lists_change_nothing(gpu_ctx, n_spheres, seed, depth, w, h):
+    """RT_OPT_ORIGIN_LISTS (secondary rays leaving a sphere test its
+    precomputed candidate list instead of walking the BVH, rt_internal.h
+    kOListSlots) gives bit-identical frames, against the BVH walk and the
+    oracle: the lists hold every sphere such a ray can hit and the closest
+    hit is order-independent (raytrace_compute.glsl:738-782)."""
+    objs = scenes.bench_objects(n_spheres, seed=seed)
+    view = rt.make_view(None, 0.37 * seed)
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        gpu_ctx.set_origin_lists(True)
+        on = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+        gpu_ctx.set_origin_lists(False)
+        off = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+    finally:
+        gpu_ctx.set_origin_lists(True)
+        sc.close()
+    assert np.array_equal(on, off, equal_nan=True), parity_stats(on, off)
+    o = oracle_render(objs, w, h, depth, t=0.37 * seed)
+    assert np.array_equal(on, o), parity_stats(on, o)
+
+
 def test_degenerate_spheres_do_not_break_the_bvh(gpu_ctx):
     objs = scenes.bench_objects(40, seed=5)
     objs[3].radius = float("nan")
