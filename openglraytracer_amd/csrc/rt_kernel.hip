@@ -445,50 +445,22 @@ __device__ __forceinline__ v3 exits(const BoxRec &b, v3 rs, v3 rd) {
                 ez = exit_num(b.mins[2], b.maxs[2], rs.z, rd.z);
     return mk(fdiv(ex, rd.x), fdiv(ey, rd.y), fdiv(ez, rd.z));
 }
-// |x| in [2^-60, 2^60]: no denormal, overflow or zero in x * v_rcp(d)
-__device__ __forceinline__ bool moderate(float x) {
-    const float a = fabsf(x);
-    return a >= 0x1p-60f && a <= 0x1p60f;
-}
-// The nearest exit of a ray from strictly inside the box, t = min of the
-// three exit quotients (:690-696), and the collision record's face (:699-705:
-// x unless t equals the y, then the z exit distance). Correctly rounded
-// division is monotonic, so when the approximate quotients n * v_rcp(d)
-// (within 2^-21 of the exact ones) are apart by more than 2^-18, the nearest
-// one's exit is the nearest, no other exit equals it, and one correctly
-// rounded division gives t: bit-identical to dividing all three (exits()).
-// Lanes with two exits that close (the ray leaves through an edge) or with
-// operands out of range divide all three, as before.
-__device__ __forceinline__ float exit_t(const BoxRec &b, v3 rs, v3 rd, int &face) {
-    const float nx = exit_num(b.mins[0], b.maxs[0], rs.x, rd.x), ny = exit_num(b.mins[1], b.maxs[1], rs.y, rd.y),
-                nz = exit_num(b.mins[2], b.maxs[2], rs.z, rd.z);
-    const float px = nx * __builtin_amdgcn_rcpf(rd.x), py = ny * __builtin_amdgcn_rcpf(rd.y),
-                pz = nz * __builtin_amdgcn_rcpf(rd.z);
-    constexpr float m = 1.0f + 0x1p-18f;
-    const bool kx = px <= py && px <= pz, ky = !kx && py <= pz;
-    const float p0 = kx ? px : (ky ? py : pz);
-    const float q1 = kx ? py : px, q2 = (kx || ky) ? pz : py;  // the other two
-    const bool decisive = moderate(nx) && moderate(ny) && moderate(nz) && moderate(rd.x) && moderate(rd.y) &&
-                          moderate(rd.z) && q1 > p0 * m && q2 > p0 * m;
-    face = kx ? 0 : (ky ? 1 : 2);
-    float t = fdiv(kx ? nx : (ky ? ny : nz), kx ? rd.x : (ky ? rd.y : rd.z));
-    if (__any(!decisive)) {
-        if (!decisive) {
-            const v3 bnd = exits(b, rs, rd);
-            t = gmin(gmin(bnd.x, bnd.y), bnd.z);
-            face = box_face(t, bnd);
-        }
-    }
-    return t;
-}
 // Box t for the closest-hit loop (-1 on a miss), the collision record's face
 // (box_face of the slab distances: t1 when entering, t2 when leaving) and
 // whether the ray leaves the box. With the origin strictly inside and no
 // NaN in the direction: t_near < 0 < t_far, so t = t_far (:690-696).
+// (One correctly rounded division for the nearest exit, chosen by the
+// approximate quotients when they are apart by more than their error,
+// bit-identical, measured slower: config 2 +4.2 %, config 5 +4.9 %, config 4
+// +3.8 %, round 5, profiles/r05d_ab.log: the three v_rcp and the selects cost
+// more than the two divisions they save.)
 __device__ __forceinline__ float box_t(const BoxRec &b, v3 rs, v3 rd, bool inside, int &face, bool &leaving) {
     if (inside && not_nan(rd)) {
+        const v3 bnd = exits(b, rs, rd);
         leaving = true;
-        return exit_t(b, rs, rd, face);
+        const float t = gmin(gmin(bnd.x, bnd.y), bnd.z);
+        face = box_face(t, bnd);
+        return t;
     }
     const Slab sl = slab(b, rs, rd);
     leaving = sl.t_near < 0.0f;
