@@ -15,7 +15,8 @@ from oracle import scenes  # noqa: E402
 
 NAMES = ["rays_primary", "rays_secondary", "closest2_wave_calls", "bvh_node_tests", "bvh_wave_iters",
          "bvh_leaf_visits", "primary_sphere_tests", "shadow_queries", "shadow_exact_tests", "gmask_wave_iters",
-         "occluded_wave_calls", "trace_wave_iters", "dmask_wave_iters", "closest1_wave_calls", "-", "-"]
+         "occluded_wave_calls", "trace_wave_iters", "dmask_wave_iters", "closest1_wave_calls", "olist_wave_passes",
+         "olist_tests"]
 name = sys.argv[1]
 cfgs = sys.argv[2:] or ["config2", "config3", "config4"]
 rt.LIB_PATH = os.path.join(ROOT, "_ab", name, "libopenglraytracer_amd.so")
