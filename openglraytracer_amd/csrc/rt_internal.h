@@ -211,7 +211,6 @@ struct LaunchParams {
     int32_t dmask_bytes;         // bytes per mask: 2, 4 or 8 (at most 16, 32, 64 spheres)
     int32_t off_gmask, gmask_words;  // wide masks in the blob past blob_units (not staged), 16-B units; -1: none
     int32_t off_glist;               // their candidate lists (kGListMax), 16-B units; -1: none
-    int32_t off_olist;               // secondary rays' origin-sphere candidate lists (kOListSlots), 16-B units; -1: none
     int32_t blob_units;      // blob size, 16-B units
     // Monte-Carlo accumulation (render_kernel<D, true>): samples
     // [sample0, sample0 + spp) per pixel, jittered inside the pixel when
@@ -243,6 +242,10 @@ struct LaunchParams {
     const FrameView *views_dev;
     const float4 *consts_dev;
     float4 frame_consts[kMaxFrameConsts];
+    // secondary rays' origin-sphere candidate lists (kOListSlots), 16-B units;
+    // -1: none (last: the depth-0/1 kernels, which never read it, keep their
+    // argument layout)
+    int32_t off_olist;
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
 // MI355X); this block stays under 6 KiB.

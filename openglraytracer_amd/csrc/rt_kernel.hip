@@ -445,28 +445,25 @@ __device__ __forceinline__ v3 exits(const BoxRec &b, v3 rs, v3 rd) {
                 ez = exit_num(b.mins[2], b.maxs[2], rs.z, rd.z);
     return mk(fdiv(ex, rd.x), fdiv(ey, rd.y), fdiv(ez, rd.z));
 }
-// Box t for the closest-hit loop (-1 on a miss), the collision record's face
-// (box_face of the slab distances: t1 when entering, t2 when leaving) and
-// whether the ray leaves the box. With the origin strictly inside and no
+// Box t for the closest-hit loop (-1 on a miss), with the slab distances the
+// collision record's face test needs (bnd: t1 when entering, t2 when leaving)
+// and whether the ray leaves the box. With the origin strictly inside and no
 // NaN in the direction: t_near < 0 < t_far, so t = t_far (:690-696).
 // (One correctly rounded division for the nearest exit, chosen by the
 // approximate quotients when they are apart by more than their error,
 // bit-identical, measured slower: config 2 +4.2 %, config 5 +4.9 %, config 4
 // +3.8 %, round 5, profiles/r05d_ab.log: the three v_rcp and the selects cost
 // more than the two divisions they save.)
-__device__ __forceinline__ float box_t(const BoxRec &b, v3 rs, v3 rd, bool inside, int &face, bool &leaving) {
+__device__ __forceinline__ float box_t(const BoxRec &b, v3 rs, v3 rd, bool inside, v3 &bnd, bool &leaving) {
     if (inside && not_nan(rd)) {
-        const v3 bnd = exits(b, rs, rd);
+        bnd = exits(b, rs, rd);
         leaving = true;
-        const float t = gmin(gmin(bnd.x, bnd.y), bnd.z);
-        face = box_face(t, bnd);
-        return t;
+        return gmin(gmin(bnd.x, bnd.y), bnd.z);
     }
     const Slab sl = slab(b, rs, rd);
     leaving = sl.t_near < 0.0f;
-    const float t = slab_t(sl);
-    face = box_face(t, sel(leaving, sl.t2, sl.t1));
-    return t;
+    bnd = sel(leaving, sl.t2, sl.t1);
+    return slab_t(sl);
 }
 // fl(num / d) < 1 for a non-negative quotient, dividing only when |num| is
 // within 2^-16 of |d| (correctly rounded division is monotonic).
@@ -650,10 +647,10 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
             rs = xform_point(B.w2l, r.start);
             inside = strictly_inside(B, rs);
         }
-        int face;
+        v3 bnd;
         bool leaving;
-        const float t = box_t(B, rs, box_dir(B, r.dir), inside, face, leaving);
-        if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, (leaving ? 1 : 0) | (face << 1)};
+        const float t = box_t(B, rs, box_dir(B, r.dir), inside, bnd, leaving);
+        if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, (leaving ? 1 : 0) | (box_face(t, bnd) << 1)};
     }
     const v3 d2 = muls(r.dir, 2.0f);
     const float qa = dot(r.dir, r.dir);
