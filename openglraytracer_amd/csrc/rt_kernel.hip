@@ -1346,16 +1346,19 @@ template <int kDepth, class Emit>
 __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active, Emit &&emit) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
     Frames<kDepth> F;
-    int level = 0;
+    // the lane's level in its tree (bits 0-7) and, from depth 2, the sphere
+    // slot + 1 its ray starts on (bits 8-: 0 for the camera or a box), in one
+    // register (a separate origin register spilled 8 B more per lane at the
+    // 80-VGPR cap)
+    int lv = 0;
     bool done = !active;
     bool first = true;
-    int origin = -1;  // the sphere slot the lane's ray starts on (-1: the camera or a box)
     while (__any(!done)) {
         RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
         const bool valid = !done;
         const bool primary = first;
         // (origin lists: depth >= 2 only, S.olist)
-        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid, kDepth >= 2 ? origin : -1);
+        const Hit h = first ? closest<true>(S, ray, valid) : closest<false>(S, ray, valid, kDepth >= 2 ? (lv >> 8) - 1 : -1);
         first = false;
         const bool hit = valid && h.obj >= 0;
         const Collision c = primary ? resolve<true>(S, ray, h, hit) : resolve<false>(S, ray, h, hit);
@@ -1366,6 +1369,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
 #endif
         if (!valid) continue;
         const MatRec &m = S.mat[c.material];
+        const int level = lv & 0xFF;
         const bool sr = hit && level < kDepth && m.reflectivity > 0.0f;
         const bool st = hit && level < kDepth && m.transparency > 0.0f;
         if (sr || st) {  // push this node, descend into its first child
@@ -1385,7 +1389,6 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
             const int here = h.slot >= 0 ? h.slot : -1;
             fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3) | (kDepth >= 2 ? (here + 1) << 11 : 0);
             F.set(level, fr);
-            if constexpr (kDepth >= 2) origin = here;
             if (sr) {
                 ray.start = add(c.p, muls(c.n, 0.001f));
                 ray.dir = reflect(ray.dir, c.n);
@@ -1393,32 +1396,32 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
                 ray.start = fr.rs;
                 ray.dir = fr.rd;
             }
-            ++level;
+            lv = kDepth >= 2 ? ((here + 1) << 8) | (level + 1) : level + 1;
             continue;
         }
         // this node is finished: fold its colour into its ancestors
         v3 value = hit ? col : black;
         bool next_child = false;
-        while (level > 0 && !next_child) {
-            Frame fr = F.get(level - 1);
+        while ((lv & 0xFF) > 0 && !next_child) {
+            Frame fr = F.get((lv & 0xFF) - 1);
             const MatRec &fm = S.mat[(fr.flags >> 3) & 0xFF];
             const float rho = fm.reflectivity, tau = fm.transparency;
             if (fr.flags & 2) {
                 fr.col = mix(fr.col, value, rho);
                 if (fr.flags & 1) {  // the refraction child comes next
                     fr.flags = (fr.flags & ~7) | 4;
-                    F.set(level - 1, fr);
+                    F.set((lv & 0xFF) - 1, fr);
                     ray.start = fr.rs;
                     ray.dir = fr.rd;
-                    if constexpr (kDepth >= 2) origin = (fr.flags >> 11) - 1;
+                    if constexpr (kDepth >= 2) lv = (lv & 0xFF) | ((fr.flags >> 11) << 8);
                     next_child = true;
                 } else {
                     value = fr.col;
-                    --level;
+                    --lv;
                 }
             } else {
                 value = mix(fr.col, value, tau);
-                --level;
+                --lv;
             }
         }
         if (!next_child) {

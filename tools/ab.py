@@ -61,6 +61,9 @@ libs = {b: load(b) for b in builds}
 # AB_ALLOW_SPILL=1 says its prediction accounts for it
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import resources  # noqa: E402
+if os.environ.get("AB_PREDICTION"):
+    # the change each variant is expected to make, stated before it is timed
+    print("# prediction: %s" % os.environ["AB_PREDICTION"], flush=True)
 for b in builds:
     print(resources.report(b.split(":")[0])[1], flush=True)
 for b in builds[1:]:
