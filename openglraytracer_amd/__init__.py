@@ -228,6 +228,11 @@ class Context:
         precomputed candidate list instead of walking the BVH (output identical)."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_ORIGIN_LISTS, 1 if on else 0))
 
+    def set_scene_shapes(self, on):
+        """RT_OPT_SCENE_SHAPES: depth-0 renders of LDS-mask scenes run the
+        kernel compiled for the scene's shape (output identical)."""
+        _check(lib().rt_context_set(self._h, abi.RT_OPT_SCENE_SHAPES, 1 if on else 0))
+
     def set_output(self, fmt):
         """RT_OPT_OUTPUT: abi.RT_OUTPUT_RGBA32F (float4 per pixel),
         abi.RT_OUTPUT_RGBA8 (the shipped GL_RGBA8 surface, 4 bytes per pixel)

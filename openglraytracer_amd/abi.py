@@ -23,6 +23,7 @@ RT_OPT_TIMING = 2
 RT_OPT_OUTPUT = 3
 RT_OPT_FRAME_CONSTS = 4
 RT_OPT_ORIGIN_LISTS = 7
+RT_OPT_SCENE_SHAPES = 8
 RT_OUTPUT_RGBA32F = 0
 RT_OUTPUT_RGBA8 = 1
 RT_OUTPUT_RGB32F = 2

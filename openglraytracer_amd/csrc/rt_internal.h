@@ -246,10 +246,22 @@ struct LaunchParams {
     // -1: none (last: the depth-0/1 kernels, which never read it, keep their
     // argument layout)
     int32_t off_olist;
+    // host only (the kernels never read it): 1 when every view of the launch
+    // culls, so the depth-0 kernels may take the scene's shape (scene_shape)
+    int32_t shape_cull;
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
 // MI355X); this block stays under 6 KiB.
 static_assert(sizeof(LaunchParams) <= 6144, "kernel argument block");
+// Scene shapes of the depth-0 kernels (render_kernel<0, ..., kShape>): the
+// scene's features that decide the path a ray takes, as compile-time
+// constants, so the kernel carries none of their run-time tests. kShape = the
+// LDS direction masks' bytes (2, 4, 8; culling on, so every shadow query
+// walks them) | kShapeOneBox (exactly one box); 0: everything read at run
+// time. The shape is the scene's, chosen per launch on the host (scene_shape).
+constexpr int kShapeMaskBytes = 15;
+constexpr int kShapeOneBox = 16;
+int scene_shape(const LaunchParams &p);
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
 constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
 constexpr int kSchedInts = 2 * kQueues * kQueueStride; // heads + done counters of one launch
@@ -331,6 +343,7 @@ struct rt_context {
     int output = RT_OUTPUT_RGBA32F;  // RT_OPT_OUTPUT
     int host_consts = 1;  // RT_OPT_FRAME_CONSTS
     int origin_lists = 1;  // RT_OPT_ORIGIN_LISTS
+    int scene_shapes = 1;  // RT_OPT_SCENE_SHAPES
     // device-side view batches (> kMaxViews views): per slot a device buffer,
     // its pinned host staging and an event after the last launch that read it
     void *batch_dev[rtamd::kBatchSlots] = {};

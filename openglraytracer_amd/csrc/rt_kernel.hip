@@ -1642,10 +1642,20 @@ __device__ __forceinline__ Ray camera_ray(const LaunchParams &p, const FrameView
 // One 8x8 wave tile (wx, wy) of view z: lane l renders pixel (8 wx + l % 8,
 // 8 wy + l / 8). `pre`: the lane's camera ray, already computed (the tiled
 // path computes it while the scene is staged), or nullptr.
-template <int kDepth, bool kAccum>
+template <int kDepth, bool kAccum, int kShape>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
+    if constexpr (kShape != 0) {
+        // the scene's shape as constants (launch_kernel checked it): every
+        // feature test on the path folds, every loop over boxes with it
+        static_assert(kDepth == 0, "scene shapes: depth-0 kernels only (no secondary rays, no BVH walk)");
+        S.cull = 1;
+        S.dmask_bytes = kShape & kShapeMaskBytes;
+        S.cone = nullptr;
+        S.nbvh = 0;
+        if constexpr ((kShape & kShapeOneBox) != 0) S.nb = 1;
+    }
     RT_CYC(kCycRaygen);
     if (!__any(px.active)) return;
     const int x = px.x, y = px.y, local_row = px.local_row;
@@ -1736,7 +1746,7 @@ constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 // frame constants come from the context's device buffer (p.views_dev,
 // p.consts_dev) instead of the kernel arguments; the view is read through
 // the constant address space (scalar loads, as the kernel arguments are).
-template <int kDepth, bool kAccum, bool kDev = false>
+template <int kDepth, bool kAccum, bool kDev = false, int kShape = 0>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     const bool queued = kQueuedDepth(kDepth) && !kDev && p.sched != nullptr;
@@ -1864,7 +1874,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
             St.sph_px = reinterpret_cast<const int4 *>(St.sph_cam + p.n_spheres);
             St.box_cam = reinterpret_cast<const float4 *>(St.sph_px + p.n_spheres);
         }
-        render_wave_tile<kDepth, kAccum>(p, St, queued ? p.view[zt] : V, wx, wy, zt,
+        render_wave_tile<kDepth, kAccum, kShape>(p, St, queued ? p.view[zt] : V, wx, wy, zt,
                                               queued ? wave_pixel(p, wx, wy) : own, own_ray, !(queued || kAccum));
         t = queued ? (q_waves + __builtin_amdgcn_readfirstlane(nxt)) * kQueues + q : total;
     }
@@ -1937,10 +1947,10 @@ int queued_views_for(const void *fn, const LaunchParams &p) {
     return n;
 }
 
-template <int kDepth, bool kAccum, bool kDev = false>
+template <int kDepth, bool kAccum, bool kDev = false, int kShape = 0>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     size_t lds = lds_bytes(p);
-    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum, kDev>);
+    const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum, kDev, kShape>);
     dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, p.n_views);
     const int wave_tiles = ((p.width + 7) / 8) * ((p.slice_rows + 7) / 8) * p.n_views;
     const int resident = p.n_cu > 0 ? groups_per_cu(fn, lds) * p.n_cu : 0;
@@ -1958,22 +1968,46 @@ hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
     } else {
         p.sched = nullptr;
     }
-    hipLaunchKernelGGL((render_kernel<kDepth, kAccum, kDev>), grid, dim3(kThreads), lds, stream, p);
+    hipLaunchKernelGGL((render_kernel<kDepth, kAccum, kDev, kShape>), grid, dim3(kThreads), lds, stream, p);
     return hipGetLastError();
+}
+
+// The depth-0 kernels in the scene's shape (scene_shape): 2-, 4- or 8-byte
+// LDS masks, one box or several; anything else runs the general kernel.
+template <bool kAccum, bool kDev>
+hipError_t launch_depth0(LaunchParams &p, hipStream_t stream) {
+    switch (scene_shape(p)) {
+        case 2: return launch_kernel<0, kAccum, kDev, 2>(p, stream);
+        case 4: return launch_kernel<0, kAccum, kDev, 4>(p, stream);
+        case 8: return launch_kernel<0, kAccum, kDev, 8>(p, stream);
+        case 2 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 2 | kShapeOneBox>(p, stream);
+        case 4 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 4 | kShapeOneBox>(p, stream);
+        case 8 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 8 | kShapeOneBox>(p, stream);
+        default: return launch_kernel<0, kAccum, kDev, 0>(p, stream);
+    }
 }
 
 template <int kDepth>
 hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
     if (p.views_dev) {  // a device-side view batch (render_batch_impl: depth 0-1, no accumulation)
-        if constexpr (kDepth <= 1) {
+        if constexpr (kDepth == 0) {
+            if (p.spp == 0) return launch_depth0<false, true>(p, stream);
+        } else if constexpr (kDepth == 1) {
             if (p.spp == 0) return launch_kernel<kDepth, false, true>(p, stream);
         }
         return hipErrorInvalidValue;
     }
+    if constexpr (kDepth == 0) return p.spp > 0 ? launch_depth0<true, false>(p, stream) : launch_depth0<false, false>(p, stream);
     return p.spp > 0 ? launch_kernel<kDepth, true>(p, stream) : launch_kernel<kDepth, false>(p, stream);
 }
 
 }  // namespace
+
+int scene_shape(const LaunchParams &p) {
+    if (!p.shape_cull || p.off_dmask < 0) return 0;  // culling off for a view, or no LDS masks
+    if (p.dmask_bytes != 2 && p.dmask_bytes != 4 && p.dmask_bytes != 8) return 0;
+    return p.dmask_bytes | (p.n_boxes == 1 ? kShapeOneBox : 0);
+}
 
 size_t lds_bytes(const LaunchParams &p) {
     // blob + per-sphere camera terms (16 B) and footprint (16 B) + per-box camera terms
@@ -2060,11 +2094,17 @@ int check_kernarg_block(hipStream_t stream) {
 hipError_t allow_large_lds(size_t bytes) {
 #define RT_KFN(d) reinterpret_cast<const void *>(&render_kernel<d, false>), \
                   reinterpret_cast<const void *>(&render_kernel<d, true>)
+#define RT_SHAPES(k) reinterpret_cast<const void *>(&render_kernel<0, false, false, k>), \
+                     reinterpret_cast<const void *>(&render_kernel<0, true, false, k>),  \
+                     reinterpret_cast<const void *>(&render_kernel<0, false, true, k>)
     const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
                          RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9),
                          reinterpret_cast<const void *>(&render_kernel<0, false, true>),
-                         reinterpret_cast<const void *>(&render_kernel<1, false, true>)};
+                         reinterpret_cast<const void *>(&render_kernel<1, false, true>),
+                         RT_SHAPES(2), RT_SHAPES(4), RT_SHAPES(8),
+                         RT_SHAPES(2 | kShapeOneBox), RT_SHAPES(4 | kShapeOneBox), RT_SHAPES(8 | kShapeOneBox)};
 #undef RT_KFN
+#undef RT_SHAPES
     for (const void *f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
     (void)hipGetLastError();  // do not leak a sticky error into the next launch check

@@ -495,6 +495,43 @@ def test_origin_lists_change_nothing(gpu_ctx, n_spheres, seed, depth, w, h):
     assert np.array_equal(on, o), parity_stats(on, o)
 
 
+@pytest.mark.parametrize("n_spheres,n_boxes,seed,w,h", [(16, 1, 0, 1920, 1080), (4, 1, 2, 320, 180),
+                                                         (32, 1, 5, 320, 180), (64, 1, 1, 320, 180),
+                                                         (16, 3, 3, 320, 180), (48, 2, 4, 256, 144)])
+def test_scene_shapes_change_nothing(gpu_ctx, n_spheres, n_boxes, seed, w, h):
+    """RT_OPT_SCENE_SHAPES (depth-0 renders of LDS-mask scenes run a kernel
+    compiled for the scene's mask width and box count, rt_internal.h
+    kShapeOneBox) gives bit-identical frames against the general kernel and
+    the oracle, for 2-, 4- and 8-byte masks, one box and several, as single
+    frames, a device-buffer batch and Monte-Carlo sums."""
+    objs = scenes.bench_objects(n_spheres, seed=seed)
+    for k in range(1, n_boxes):  # more boxes: small rotated cubes among the spheres
+        objs.append(scenes.box((-0.5, -0.5, -0.5), (0.5, 0.5, 0.5), (2.0 * k - 3.0, -4.0, 1.5 * k),
+                               (0.0, 30.0 * k, 0.0), k % 7))
+    views = [rt.make_view(None, 0.25 * k + 0.1 * seed) for k in range(10)]
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        out = {}
+        for on in (True, False):
+            gpu_ctx.set_scene_shapes(on)
+            single = rt.render(gpu_ctx, sc, w, h, 0, view=views[0])
+            batch = torch.empty((len(views), h, w, 4), dtype=torch.float32, device="cuda")
+            rt.render_batch(gpu_ctx, sc, batch.data_ptr(), w, h, 0, views)  # > 8 views: the device-buffer kernel
+            acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda")
+            rt.render_accumulate(gpu_ctx, sc, acc.data_ptr(), w, h, 0, 3, 0, seed=seed, view=views[0])
+            torch.cuda.synchronize()
+            out[on] = (single, batch.cpu().numpy(), acc.cpu().numpy())
+    finally:
+        gpu_ctx.set_scene_shapes(True)
+        sc.close()
+    for a, b in zip(out[True], out[False]):
+        assert np.array_equal(a, b, equal_nan=True), parity_stats(a, b)
+    assert np.array_equal(out[True][1][0], out[True][0])
+    rows = (h // 2, h // 2 + 2)
+    o = port.render(objs, w, h, 0, 0.1 * seed, rows=rows)
+    assert np.array_equal(out[True][0][rows[0]:rows[1]], o), parity_stats(out[True][0][rows[0]:rows[1]], o)
+
+
 def test_degenerate_spheres_do_not_break_the_bvh(gpu_ctx):
     objs = scenes.bench_objects(40, seed=5)
     objs[3].radius = float("nan")

@@ -41,11 +41,15 @@ def lib_path(spec):
 
 
 def kernel_name(mangled):
-    """render_kernel<D, MC, DEV> from the mangled name, else the mangled name."""
-    m = re.search(r"render_kernelILi(\d)ELb([01])ELb([01])E", mangled)
+    """render_kernel<D, MC, DEV[, SHAPE]> from the mangled name (SHAPE: the
+    depth-0 scene shapes, rt_internal.h kShapeOneBox), else the mangled name."""
+    m = re.search(r"render_kernelILi(\d)ELb([01])ELb([01])E(?:Li(\d+)E)?", mangled)
     if m:
-        return "render_kernel<%s,%s,%s>" % (m.group(1), "true" if m.group(2) == "1" else "false",
-                                            "true" if m.group(3) == "1" else "false")
+        name = "render_kernel<%s,%s,%s" % (m.group(1), "true" if m.group(2) == "1" else "false",
+                                           "true" if m.group(3) == "1" else "false")
+        if m.group(4) and m.group(4) != "0":
+            name += ",%s" % m.group(4)
+        return name + ">"
     return mangled
 
 
