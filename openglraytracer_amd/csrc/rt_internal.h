@@ -253,15 +253,18 @@ struct LaunchParams {
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
 // MI355X); this block stays under 6 KiB.
 static_assert(sizeof(LaunchParams) <= 6144, "kernel argument block");
-// Scene shapes of the depth-0 kernels (render_kernel<0, ..., kShape>): the
-// scene's features that decide the path a ray takes, as compile-time
-// constants, so the kernel carries none of their run-time tests. kShape = the
-// LDS direction masks' bytes (2, 4, 8; culling on, so every shadow query
-// walks them) | kShapeOneBox (exactly one box); 0: everything read at run
-// time. The shape is the scene's, chosen per launch on the host (scene_shape).
+// Scene shapes (render_kernel<D, ..., kShape>): the scene's features that
+// decide the path a ray takes, as compile-time constants, so the kernel
+// carries none of their run-time tests. Depth 0: the LDS direction masks'
+// bytes (2, 4, 8; culling on, so every shadow query walks them). Depth >= 2:
+// kShapeWide (culling on; wide masks with their candidate lists and the
+// origin-sphere lists present). Either | kShapeOneBox (exactly one box).
+// 0: everything read at run time. Chosen per launch on the host
+// (scene_shape), like the reference's shader, compiled for its own scene.
 constexpr int kShapeMaskBytes = 15;
 constexpr int kShapeOneBox = 16;
-int scene_shape(const LaunchParams &p);
+constexpr int kShapeWide = 32;
+int scene_shape(const LaunchParams &p, int max_depth);
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
 constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
 constexpr int kSchedInts = 2 * kQueues * kQueueStride; // heads + done counters of one launch

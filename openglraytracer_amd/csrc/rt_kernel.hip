@@ -1646,16 +1646,28 @@ template <int kDepth, bool kAccum, int kShape>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
-    if constexpr (kShape != 0) {
-        // the scene's shape as constants (launch_kernel checked it): every
-        // feature test on the path folds, every loop over boxes with it
-        static_assert(kDepth == 0, "scene shapes: depth-0 kernels only (no secondary rays, no BVH walk)");
+    // the scene's shape as constants (scene_shape checked it on the host):
+    // every feature test on the path folds, and with one box every loop over
+    // the boxes
+    if constexpr ((kShape & kShapeMaskBytes) != 0) {
+        // depth 0: the shadow queries walk LDS direction masks
+        static_assert(kDepth == 0, "LDS-mask shapes: depth-0 kernels (no secondary rays, no BVH walk)");
         S.cull = 1;
         S.dmask_bytes = kShape & kShapeMaskBytes;
         S.cone = nullptr;
         S.nbvh = 0;
-        if constexpr ((kShape & kShapeOneBox) != 0) S.nb = 1;
     }
+    if constexpr ((kShape & kShapeWide) != 0) {
+        // depth >= 2: wide masks with their candidate lists, origin-sphere lists
+        static_assert(kDepth >= 2, "wide shapes: the recursive kernels");
+        S.cull = 1;
+        S.dmask = nullptr;
+        S.cone = nullptr;
+        __builtin_assume(S.gmask != nullptr);
+        __builtin_assume(S.glist != nullptr);
+        __builtin_assume(S.olist != nullptr);
+    }
+    if constexpr ((kShape & kShapeOneBox) != 0) S.nb = 1;
     RT_CYC(kCycRaygen);
     if (!__any(px.active)) return;
     const int x = px.x, y = px.y, local_row = px.local_row;
@@ -1976,7 +1988,7 @@ hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
 // LDS masks, one box or several; anything else runs the general kernel.
 template <bool kAccum, bool kDev>
 hipError_t launch_depth0(LaunchParams &p, hipStream_t stream) {
-    switch (scene_shape(p)) {
+    switch (scene_shape(p, 0)) {
         case 2: return launch_kernel<0, kAccum, kDev, 2>(p, stream);
         case 4: return launch_kernel<0, kAccum, kDev, 4>(p, stream);
         case 8: return launch_kernel<0, kAccum, kDev, 8>(p, stream);
@@ -1984,6 +1996,16 @@ hipError_t launch_depth0(LaunchParams &p, hipStream_t stream) {
         case 4 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 4 | kShapeOneBox>(p, stream);
         case 8 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 8 | kShapeOneBox>(p, stream);
         default: return launch_kernel<0, kAccum, kDev, 0>(p, stream);
+    }
+}
+
+// The recursive kernels in the wide-mask shape (scene_shape), else general.
+template <int kDepth>
+hipError_t launch_deep(LaunchParams &p, hipStream_t stream) {
+    switch (scene_shape(p, kDepth)) {
+        case kShapeWide: return launch_kernel<kDepth, false, false, kShapeWide>(p, stream);
+        case kShapeWide | kShapeOneBox: return launch_kernel<kDepth, false, false, kShapeWide | kShapeOneBox>(p, stream);
+        default: return launch_kernel<kDepth, false, false, 0>(p, stream);
     }
 }
 
@@ -1998,15 +2020,26 @@ hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
         return hipErrorInvalidValue;
     }
     if constexpr (kDepth == 0) return p.spp > 0 ? launch_depth0<true, false>(p, stream) : launch_depth0<false, false>(p, stream);
+    if constexpr (kDepth >= 2) {
+        if (p.spp == 0) return launch_deep<kDepth>(p, stream);
+    }
     return p.spp > 0 ? launch_kernel<kDepth, true>(p, stream) : launch_kernel<kDepth, false>(p, stream);
 }
 
 }  // namespace
 
-int scene_shape(const LaunchParams &p) {
-    if (!p.shape_cull || p.off_dmask < 0) return 0;  // culling off for a view, or no LDS masks
-    if (p.dmask_bytes != 2 && p.dmask_bytes != 4 && p.dmask_bytes != 8) return 0;
-    return p.dmask_bytes | (p.n_boxes == 1 ? kShapeOneBox : 0);
+int scene_shape(const LaunchParams &p, int max_depth) {
+    if (!p.shape_cull) return 0;  // culling off for a view (or RT_OPT_SCENE_SHAPES 0)
+    const int box = p.n_boxes == 1 ? kShapeOneBox : 0;
+    if (max_depth == 0) {  // every shadow query walks the LDS masks
+        if (p.off_dmask < 0 || (p.dmask_bytes != 2 && p.dmask_bytes != 4 && p.dmask_bytes != 8)) return 0;
+        return p.dmask_bytes | box;
+    }
+    if (max_depth >= 2) {  // the wide masks' lists and the origin-sphere lists take the rays
+        if (p.off_gmask < 0 || p.off_glist < 0 || p.off_olist < 0) return 0;
+        return kShapeWide | box;
+    }
+    return 0;
 }
 
 size_t lds_bytes(const LaunchParams &p) {
@@ -2097,14 +2130,18 @@ hipError_t allow_large_lds(size_t bytes) {
 #define RT_SHAPES(k) reinterpret_cast<const void *>(&render_kernel<0, false, false, k>), \
                      reinterpret_cast<const void *>(&render_kernel<0, true, false, k>),  \
                      reinterpret_cast<const void *>(&render_kernel<0, false, true, k>)
+#define RT_WIDE(d) reinterpret_cast<const void *>(&render_kernel<d, false, false, kShapeWide>), \
+                   reinterpret_cast<const void *>(&render_kernel<d, false, false, kShapeWide | kShapeOneBox>)
     const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
                          RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9),
                          reinterpret_cast<const void *>(&render_kernel<0, false, true>),
                          reinterpret_cast<const void *>(&render_kernel<1, false, true>),
                          RT_SHAPES(2), RT_SHAPES(4), RT_SHAPES(8),
-                         RT_SHAPES(2 | kShapeOneBox), RT_SHAPES(4 | kShapeOneBox), RT_SHAPES(8 | kShapeOneBox)};
+                         RT_SHAPES(2 | kShapeOneBox), RT_SHAPES(4 | kShapeOneBox), RT_SHAPES(8 | kShapeOneBox),
+                         RT_WIDE(2), RT_WIDE(3), RT_WIDE(4), RT_WIDE(5), RT_WIDE(6), RT_WIDE(7), RT_WIDE(8), RT_WIDE(9)};
 #undef RT_KFN
 #undef RT_SHAPES
+#undef RT_WIDE
     for (const void *f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
     (void)hipGetLastError();  // do not leak a sticky error into the next launch check

@@ -532,6 +532,40 @@ def test_scene_shapes_change_nothing(gpu_ctx, n_spheres, n_boxes, seed, w, h):
     assert np.array_equal(out[True][0][rows[0]:rows[1]], o), parity_stats(out[True][0][rows[0]:rows[1]], o)
 
 
+@pytest.mark.parametrize("n_spheres,n_boxes,seed,depth,w,h", [(64, 1, 0, 2, 480, 270), (256, 1, 1, 4, 320, 180),
+                                                               (100, 2, 2, 3, 320, 180), (33, 1, 3, 9, 160, 90),
+                                                               (200, 3, 4, 5, 256, 144)])
+def test_wide_scene_shapes_change_nothing(gpu_ctx, n_spheres, n_boxes, seed, depth, w, h):
+    """RT_OPT_SCENE_SHAPES for the recursive kernels (scenes whose shadow
+    queries walk the wide masks' candidate lists and whose secondary rays the
+    origin-sphere lists take, one box or several, rt_internal.h kShapeWide):
+    bit-identical frames against the general kernel and the oracle, single
+    frames and a batch of views in one queued launch."""
+    objs = scenes.bench_objects(n_spheres, seed=seed)
+    for k in range(1, n_boxes):
+        objs.append(scenes.box((-0.5, -0.5, -0.5), (0.5, 0.5, 0.5), (2.0 * k - 3.0, -4.0, 1.5 * k),
+                               (0.0, 30.0 * k, 0.0), k % 7))
+    views = [rt.make_view(None, 0.3 * k + 0.1 * seed) for k in range(3)]
+    sc = rt.Scene(gpu_ctx, objs)
+    try:
+        out = {}
+        for on in (True, False):
+            gpu_ctx.set_scene_shapes(on)
+            single = rt.render(gpu_ctx, sc, w, h, depth, view=views[0])
+            batch = torch.empty((len(views), h, w, 4), dtype=torch.float32, device="cuda")
+            rt.render_batch(gpu_ctx, sc, batch.data_ptr(), w, h, depth, views)
+            torch.cuda.synchronize()
+            out[on] = (single, batch.cpu().numpy())
+    finally:
+        gpu_ctx.set_scene_shapes(True)
+        sc.close()
+    for a, b in zip(out[True], out[False]):
+        assert np.array_equal(a, b, equal_nan=True), parity_stats(a, b)
+    assert np.array_equal(out[True][1][0], out[True][0])
+    o = oracle_render(objs, w, h, depth, t=0.1 * seed)
+    assert np.array_equal(out[True][0], o), parity_stats(out[True][0], o)
+
+
 def test_degenerate_spheres_do_not_break_the_bvh(gpu_ctx):
     objs = scenes.bench_objects(40, seed=5)
     objs[3].radius = float("nan")
