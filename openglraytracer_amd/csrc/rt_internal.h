@@ -262,6 +262,7 @@ static_assert(sizeof(LaunchParams) <= 6144, "kernel argument block");
 // 0: everything read at run time. Chosen per launch on the host
 // (scene_shape), like the reference's shader, compiled for its own scene.
 constexpr int kShapeMaskBytes = 15;
+constexpr int kShapeMaskTexels = 12;  // the LDS masks' texels per face edge in a depth-0 shape (rt_scene.cpp picks 12 where it fits)
 constexpr int kShapeOneBox = 16;
 constexpr int kShapeWide = 32;
 int scene_shape(const LaunchParams &p, int max_depth);

@@ -1656,6 +1656,10 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         S.dmask_bytes = kShape & kShapeMaskBytes;
         S.cone = nullptr;
         S.nbvh = 0;
+        S.dmask_n = kShapeMaskTexels;
+        // LDS masks exist for 1..kMaskMaxSpheres spheres: one pass of the
+        // primary rays' 64-lane footprint test
+        __builtin_assume(S.ns > 0 && S.ns <= kMaskMaxSpheres);
     }
     if constexpr ((kShape & kShapeWide) != 0) {
         // depth >= 2: wide masks with their candidate lists, origin-sphere lists
@@ -2032,7 +2036,9 @@ int scene_shape(const LaunchParams &p, int max_depth) {
     if (!p.shape_cull) return 0;  // culling off for a view (or RT_OPT_SCENE_SHAPES 0)
     const int box = p.n_boxes == 1 ? kShapeOneBox : 0;
     if (max_depth == 0) {  // every shadow query walks the LDS masks
-        if (p.off_dmask < 0 || (p.dmask_bytes != 2 && p.dmask_bytes != 4 && p.dmask_bytes != 8)) return 0;
+        if (p.off_dmask < 0 || (p.dmask_bytes != 2 && p.dmask_bytes != 4 && p.dmask_bytes != 8) ||
+            p.dmask_n != kShapeMaskTexels)
+            return 0;
         return p.dmask_bytes | box;
     }
     if (max_depth >= 2) {  // the wide masks' lists and the origin-sphere lists take the rays
