@@ -72,6 +72,13 @@ __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + (a.y * b.y
 #define RT_FAST_POW
 #endif
 
+// Wave votes on the lane masks themselves: the ballot of the condition (its
+// compare's lane mask, without HIP's __any/__all round trip of the predicate
+// through a 0/1 vector register and a second compare) against zero / exec.
+__device__ __forceinline__ bool wave_any(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
+__device__ __forceinline__ bool wave_all(bool c) { return __builtin_amdgcn_ballot_w64(c) == __builtin_amdgcn_read_exec(); }
+__device__ __forceinline__ uint64_t wave_ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
 // ---- correctly rounded division and square root, short forms -------------
 // hipcc lowers a / b (IEEE) to div_scale(b), rcp, 2 fma (the refined
 // reciprocal r), div_scale(a), mul, 3 fma, div_fmas, div_fixup; and sqrtf(x)
@@ -127,7 +134,11 @@ __device__ __forceinline__ float inv_sqrt(float d) {
 #ifdef RT_FAST_RSQ
     return __builtin_amdgcn_rsqf(d);
 #endif
-    if (__all(d >= 0x1p-96f && d <= 0x1p100f)) return rcp_refined(sqrt_short(d)).r;
+    // d in [2^-96, 2^100] as one unsigned compare of the bit pattern (NaN and
+    // negative d fall outside), so the vote takes the compare's lane mask
+    if (wave_all(__float_as_uint(d) - __float_as_uint(0x1p-96f) <=
+                 __float_as_uint(0x1p100f) - __float_as_uint(0x1p-96f)))
+        return rcp_refined(sqrt_short(d)).r;
     return 1.0f / sqrtf(d);
 }
 // normalize(v) = v * inversesqrt(dot(v, v))
@@ -156,7 +167,7 @@ __device__ __forceinline__ v3 normalize_unit(v3 a) {
 #ifdef RT_FAST_RSQ
     return muls(a, __builtin_amdgcn_rsqf(d));
 #endif
-    if (__all(near_one(d))) return muls(a, inv_sqrt_near_one(d));
+    if (wave_all(near_one(d))) return muls(a, inv_sqrt_near_one(d));
     return muls(a, inv_sqrt(d));
 }
 __device__ __forceinline__ float gmin(float a, float b) { return a < b ? a : b; }
@@ -527,7 +538,7 @@ __device__ __forceinline__ float sphere_sqrt(float qd) {
 #ifdef RT_FAST_SQRT
     return __builtin_amdgcn_sqrtf(qd);
 #endif
-    if (__all(qd >= 0x1p-96f)) return sqrt_short(qd);
+    if (wave_all(qd >= 0x1p-96f)) return sqrt_short(qd);
     return sqrtf(qd);
 }
 // intersect_sphere_object's t (:586-625) from the ray-invariant terms.
@@ -666,7 +677,7 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
                 const int4 bb = S.sph_px[k];
                 cand = !(bb.y < S.tx0 || bb.x > S.tx1 || bb.w < S.ty0 || bb.z > S.ty1);
             }
-            uint64_t mask = __ballot(cand);
+            uint64_t mask = wave_ballot(cand);
             while (mask) {
                 const int s = base + __builtin_ctzll(mask);
                 mask &= mask - 1;
@@ -702,7 +713,7 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
             uint32_t n = cnt < static_cast<uint32_t>(kOListSlots) ? cnt : static_cast<uint32_t>(kOListSlots);
 #pragma unroll
             for (int i = 0; i < kOListSlots; ++i) {  // i: a constant after unrolling (byte i + 1 of the record)
-                if (!__any(static_cast<uint32_t>(i) < n)) break;
+                if (!wave_any(static_cast<uint32_t>(i) < n)) break;
                 RT_STAT(14, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (i == 8 || i == 16) {  // the stored bounds of candidates 8 and 16
                     const uint32_t q = i == 8 ? (rb.z >> 16) : (rb.w & 0xFFFFu);
@@ -740,7 +751,7 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
         int held = 0;  // (count << 24) | first sphere of the held leaf
         // the ray's octant picks its traversal order (nearer child first)
         const int oct = (r.dir.x < 0.0f ? 1 : 0) | (r.dir.y < 0.0f ? 2 : 0) | (r.dir.z < 0.0f ? 4 : 0);
-        while (__any(node >= 0)) {
+        while (wave_any(node >= 0)) {
             while (node >= 0 && held == 0) {
                 RT_STAT(3, true);
                 RT_STAT(4, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
@@ -825,13 +836,13 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
         const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit);
         hit = hit | (need & occ);
     }
-    if (!__any(need && !hit)) return hit;
+    if (!wave_any(need && !hit)) return hit;
     if (S.cull && !S.gmask && S.dmask) {
         // the LDS-mask walk (see below) with the ray's quadratic terms
         // computed only when some lane of the wave has a candidate (most
         // shadow queries of a wave have none: config 2 -1 %)
         const uint64_t m64 = need && !hit ? mask : 0u;
-        if (!__any(m64 != 0u)) return hit;
+        if (!wave_any(m64 != 0u)) return hit;
         const v3 d2 = muls(dir, 2.0f);
         const float qa = dot(dir, dir);
         const float qa2 = 2.0f * qa, qa4 = 4.0f * qa;
@@ -844,7 +855,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
         };
         if (S.dmask_bytes == 8) {
             uint64_t cand = m64;
-            while (__any(cand != 0u)) {
+            while (wave_any(cand != 0u)) {
                 if (cand) {
                     test(__builtin_ctzll(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
@@ -852,7 +863,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
             }
         } else {  // 32-bit masks: half the bit arithmetic
             uint32_t cand = static_cast<uint32_t>(m64);
-            while (__any(cand != 0u)) {
+            while (wave_any(cand != 0u)) {
                 RT_STAT(12, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (cand) {
                     test(__builtin_ctz(cand));
@@ -888,7 +899,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
     };
     if (!S.cull) {
         for (int s = 0; s < S.ns; ++s) {
-            if (!__any(need && !hit)) break;
+            if (!wave_any(need && !hit)) break;
             exact(s);
         }
         return hit;
@@ -914,7 +925,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
             uint32_t cnt = rec.x & 0xFFu;
             const bool wide = need && !hit && (texel < 0 || cnt == kGListOverflow);
             if (wide) cnt = 0u;
-            for (uint32_t i = 1; __any(i <= cnt); ++i) {  // i: wave-uniform
+            for (uint32_t i = 1; wave_any(i <= cnt); ++i) {  // i: wave-uniform
                 RT_STAT(9, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (i <= cnt) {
                     const uint32_t word = i < 4 ? rec.x : (i < 8 ? rec.y : (i < 12 ? rec.z : rec.w));
@@ -922,7 +933,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
                     if (hit) cnt = 0u;
                 }
             }
-            if (!__any(wide)) return hit;
+            if (!wave_any(wide)) return hit;
             ask = wide;  // more than kGListMax candidates, or every sphere: the words
         }
         // every word of the texel requested up front (independent L2 loads
@@ -946,14 +957,14 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
                 const int rest = S.ns - 64 * w;
                 if (rest < 64) cand &= (uint64_t{1} << rest) - 1u;
             }
-            while (__any(cand != 0u)) {
+            while (wave_any(cand != 0u)) {
                 RT_STAT(9, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (cand) {
                     exact_cand(64 * w + __builtin_ctzll(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
                 }
             }
-            if (!__any(ask && !hit)) break;
+            if (!wave_any(ask && !hit)) break;
         }
         return hit;
     }
@@ -963,7 +974,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
         // lane walks its own mask (usually empty)
         if (S.dmask_bytes == 8) {
             uint64_t cand = need && !hit ? mask : 0u;
-            while (__any(cand != 0u)) {
+            while (wave_any(cand != 0u)) {
                 if (cand) {
                     exact_cand(__builtin_ctzll(cand));
                     cand = hit ? 0u : cand & (cand - 1u);
@@ -971,7 +982,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
             }
         } else {  // 32-bit masks: half the bit arithmetic
             uint32_t cand = need && !hit ? static_cast<uint32_t>(mask) : 0u;
-            while (__any(cand != 0u)) {
+            while (wave_any(cand != 0u)) {
                 RT_STAT(12, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
                 if (cand) {
                     exact_cand(__builtin_ctz(cand));
@@ -990,7 +1001,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
     const float ul = fsqrt_approx(dot(u, u));
     const v3 uh = ul > 0.0f ? muls(u, __builtin_amdgcn_rcpf(ul)) : mk(0.0f, 0.0f, 0.0f);
     // cone axis: the direction of the first active lane
-    const int lead = __builtin_ctzll(__ballot(act));
+    const int lead = __builtin_ctzll(wave_ballot(act));
     const v3 ax = mk(lane_value(uh.x, lead), lane_value(uh.y, lead), lane_value(uh.z, lead));
     const float cmin = wave_min(act ? dot(ax, uh) : 1.0f);
     const float maxlen = wave_max(act ? ul : 0.0f);
@@ -1061,12 +1072,12 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
                 cand = !(dot(ax, v) < cos_lim - 1e-3f);
             }
         }
-        uint64_t mask = __ballot(cand);
+        uint64_t mask = wave_ballot(cand);
         while (mask) {
             const int s = base + __builtin_ctzll(mask);
             mask &= mask - 1;
             exact(s);
-            if (!__any(need && !hit)) return hit;
+            if (!wave_any(need && !hit)) return hit;
         }
     }
     return hit;
@@ -1202,7 +1213,7 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
         // of LDS-loaded operands compiled to nested divergent branches
         const bool need_pow = !((xs == 0.0f) & (m.shininess > 0.0f));
         float ks = 0.0f;
-        if (__any(need_pow && valid)) ks = need_pow ? glsl_pow_cos(xs, m.shininess) : 0.0f;
+        if (wave_any(need_pow && valid)) ks = need_pow ? glsl_pow_cos(xs, m.shininess) : 0.0f;
         const float4 nd = make_float4(dif.x + q.ld_md[0] * kd, dif.y + q.ld_md[1] * kd, dif.z + q.ld_md[2] * kd,
                                       dif.w + q.ld_md[3] * kd);
         const float4 ns = make_float4(spe.x + q.ls_ms[0] * ks, spe.y + q.ls_ms[1] * ks, spe.z + q.ls_ms[2] * ks,
@@ -1217,7 +1228,7 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
         if (need) { dif = nd; spe = ns; }
         continue;
 #endif
-        if (__any(need)) {
+        if (wave_any(need)) {
             // its direction-mask texel (p - L = -sdir), looked up only where
             // some lane casts the shadow ray (ahead of the shading math, to
             // overlap the LDS read, it measured slower: config 3 0.978 vs 0.960
@@ -1276,7 +1287,7 @@ __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     const Hit h = closest<true>(S, r, valid);
     RT_PHASE(3);
     const bool hit = valid && h.obj >= 0;
-    if (!__any(hit)) return black;  // per-wave early out
+    if (!wave_any(hit)) return black;  // per-wave early out
     const Collision c = resolve<true>(S, r, h, hit);
     RT_PHASE(4);
 #ifdef RT_ABLATE_PHONG
@@ -1353,7 +1364,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
     int lv = 0;
     bool done = !active;
     bool first = true;
-    while (__any(!done)) {
+    while (wave_any(!done)) {
         RT_STAT(11, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
         const bool valid = !done;
         const bool primary = first;
@@ -1380,7 +1391,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
             // only in waves with a refraction child (every surface of the
             // bench scenes reflects, few refract: config 4 14.68 -> 14.62 ms,
             // config 3 0.881 -> 0.878 ms, r03d)
-            if (__any(st)) {
+            if (wave_any(st)) {
                 const float ratio = c.inside ? m.eta_out : m.eta_in;  // (:1013-1016, host-divided)
                 fr.rd = refract(ray.dir, c.n, ratio);
             }
@@ -1673,7 +1684,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
     }
     if constexpr ((kShape & kShapeOneBox) != 0) S.nb = 1;
     RT_CYC(kCycRaygen);
-    if (!__any(px.active)) return;
+    if (!wave_any(px.active)) return;
     const int x = px.x, y = px.y, local_row = px.local_row;
     const bool active = px.active;
     const int lr0 = p.slice_begin + wy * 8;
