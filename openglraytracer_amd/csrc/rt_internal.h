@@ -249,6 +249,7 @@ struct LaunchParams {
     // host only (the kernels never read it): 1 when every view of the launch
     // culls, so the depth-0 kernels may take the scene's shape (scene_shape)
     int32_t shape_cull;
+    int32_t scene_room;  // host only: every scene of the launch is a room (DeviceScene::room)
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
 // MI355X); this block stays under 6 KiB.
@@ -258,12 +259,13 @@ static_assert(sizeof(LaunchParams) <= 6144, "kernel argument block");
 // carries none of their run-time tests. Depth 0: the LDS direction masks'
 // bytes (2, 4, 8; culling on, so every shadow query walks them). Depth >= 2:
 // kShapeWide (culling on; wide masks with their candidate lists and the
-// origin-sphere lists present). Either | kShapeOneBox (exactly one box).
+// origin-sphere lists present). Either | kShapeRoom (exactly one box, a room:
+// translate-only, every live light inside it).
 // 0: everything read at run time. Chosen per launch on the host
 // (scene_shape), like the reference's shader, compiled for its own scene.
 constexpr int kShapeMaskBytes = 15;
 constexpr int kShapeMaskTexels = 12;  // the LDS masks' texels per face edge in a depth-0 shape (rt_scene.cpp picks 12 where it fits)
-constexpr int kShapeOneBox = 16;
+constexpr int kShapeRoom = 16;
 constexpr int kShapeWide = 32;
 int scene_shape(const LaunchParams &p, int max_depth);
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
@@ -280,6 +282,9 @@ struct DeviceScene {
     int32_t off_gmask = -1, gmask_words = 0, off_glist = -1;
     int32_t off_olist = -1;
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
+    // 1: the one box is a room: translate-only, every live light strictly
+    // inside it (the shadow queries' box shortcut always applies; kShapeRoom)
+    int32_t room = 0;
 };
 
 // rt_scene.cpp: every view's per-frame constants on the host, bit-identical

@@ -381,6 +381,7 @@ struct Scene {
     const __attribute__((address_space(4))) LightRec *clight;
     int ns, nb, nl, nm, nbvh;
     int cull;
+    int room;  // the one box is a room (kShapeRoom): its shadow shortcut always applies
     int tx0, tx1, ty0, ty1;  // this wave's pixel rectangle (frame coordinates)
 };
 
@@ -489,8 +490,8 @@ __device__ __forceinline__ bool quotient_below_one(float num, float d) {
 // Does the box hold an occluder with 0 < t < 1 (:813-816)? light_bit: the
 // light is inside the box with a margin (host, float64), so a segment that
 // starts inside ends inside too and exits past t = 1.
-__device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, uint32_t light_bit) {
-    if ((b.light_inside & light_bit) && b.translate_only) {
+__device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, uint32_t light_bit, bool room) {
+    if (room || ((b.light_inside & light_bit) && b.translate_only)) {
         // identity rotation: xform_point is ((1 x + 0 y) + 0 z) + w, which for
         // finite start equals x + w up to the sign of a zero (comparisons
         // alike); a non-finite component stays non-finite here and fails
@@ -833,7 +834,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
     for (int b = 0; b < S.nb; ++b) {
         // every lane tests (no divergent branch around the test; lanes
         // without the query or already shadowed keep their flag)
-        const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit);
+        const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit, S.room != 0);
         hit = hit | (need & occ);
     }
     if (!wave_any(need && !hit)) return hit;
@@ -1657,9 +1658,10 @@ template <int kDepth, bool kAccum, int kShape>
 __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S, const FrameView &V, int wx, int wy,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
+    S.room = 0;
     // the scene's shape as constants (scene_shape checked it on the host):
-    // every feature test on the path folds, and with one box every loop over
-    // the boxes
+    // every feature test on the path folds, and with a room (one box) every
+    // loop over the boxes and the shadow queries' box shortcut test
     if constexpr ((kShape & kShapeMaskBytes) != 0) {
         // depth 0: the shadow queries walk LDS direction masks
         static_assert(kDepth == 0, "LDS-mask shapes: depth-0 kernels (no secondary rays, no BVH walk)");
@@ -1682,7 +1684,10 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         __builtin_assume(S.glist != nullptr);
         __builtin_assume(S.olist != nullptr);
     }
-    if constexpr ((kShape & kShapeOneBox) != 0) S.nb = 1;
+    if constexpr ((kShape & kShapeRoom) != 0) {
+        S.nb = 1;
+        S.room = 1;
+    }
     RT_CYC(kCycRaygen);
     if (!wave_any(px.active)) return;
     const int x = px.x, y = px.y, local_row = px.local_row;
@@ -2007,9 +2012,9 @@ hipError_t launch_depth0(LaunchParams &p, hipStream_t stream) {
         case 2: return launch_kernel<0, kAccum, kDev, 2>(p, stream);
         case 4: return launch_kernel<0, kAccum, kDev, 4>(p, stream);
         case 8: return launch_kernel<0, kAccum, kDev, 8>(p, stream);
-        case 2 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 2 | kShapeOneBox>(p, stream);
-        case 4 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 4 | kShapeOneBox>(p, stream);
-        case 8 | kShapeOneBox: return launch_kernel<0, kAccum, kDev, 8 | kShapeOneBox>(p, stream);
+        case 2 | kShapeRoom: return launch_kernel<0, kAccum, kDev, 2 | kShapeRoom>(p, stream);
+        case 4 | kShapeRoom: return launch_kernel<0, kAccum, kDev, 4 | kShapeRoom>(p, stream);
+        case 8 | kShapeRoom: return launch_kernel<0, kAccum, kDev, 8 | kShapeRoom>(p, stream);
         default: return launch_kernel<0, kAccum, kDev, 0>(p, stream);
     }
 }
@@ -2019,7 +2024,7 @@ template <int kDepth>
 hipError_t launch_deep(LaunchParams &p, hipStream_t stream) {
     switch (scene_shape(p, kDepth)) {
         case kShapeWide: return launch_kernel<kDepth, false, false, kShapeWide>(p, stream);
-        case kShapeWide | kShapeOneBox: return launch_kernel<kDepth, false, false, kShapeWide | kShapeOneBox>(p, stream);
+        case kShapeWide | kShapeRoom: return launch_kernel<kDepth, false, false, kShapeWide | kShapeRoom>(p, stream);
         default: return launch_kernel<kDepth, false, false, 0>(p, stream);
     }
 }
@@ -2045,7 +2050,7 @@ hipError_t launch_depth(LaunchParams &p, hipStream_t stream) {
 
 int scene_shape(const LaunchParams &p, int max_depth) {
     if (!p.shape_cull) return 0;  // culling off for a view (or RT_OPT_SCENE_SHAPES 0)
-    const int box = p.n_boxes == 1 ? kShapeOneBox : 0;
+    const int box = p.n_boxes == 1 && p.scene_room ? kShapeRoom : 0;
     if (max_depth == 0) {  // every shadow query walks the LDS masks
         if (p.off_dmask < 0 || (p.dmask_bytes != 2 && p.dmask_bytes != 4 && p.dmask_bytes != 8) ||
             p.dmask_n != kShapeMaskTexels)
@@ -2148,13 +2153,13 @@ hipError_t allow_large_lds(size_t bytes) {
                      reinterpret_cast<const void *>(&render_kernel<0, true, false, k>),  \
                      reinterpret_cast<const void *>(&render_kernel<0, false, true, k>)
 #define RT_WIDE(d) reinterpret_cast<const void *>(&render_kernel<d, false, false, kShapeWide>), \
-                   reinterpret_cast<const void *>(&render_kernel<d, false, false, kShapeWide | kShapeOneBox>)
+                   reinterpret_cast<const void *>(&render_kernel<d, false, false, kShapeWide | kShapeRoom>)
     const void *fns[] = {RT_KFN(0), RT_KFN(1), RT_KFN(2), RT_KFN(3), RT_KFN(4),
                          RT_KFN(5), RT_KFN(6), RT_KFN(7), RT_KFN(8), RT_KFN(9),
                          reinterpret_cast<const void *>(&render_kernel<0, false, true>),
                          reinterpret_cast<const void *>(&render_kernel<1, false, true>),
                          RT_SHAPES(2), RT_SHAPES(4), RT_SHAPES(8),
-                         RT_SHAPES(2 | kShapeOneBox), RT_SHAPES(4 | kShapeOneBox), RT_SHAPES(8 | kShapeOneBox),
+                         RT_SHAPES(2 | kShapeRoom), RT_SHAPES(4 | kShapeRoom), RT_SHAPES(8 | kShapeRoom),
                          RT_WIDE(2), RT_WIDE(3), RT_WIDE(4), RT_WIDE(5), RT_WIDE(6), RT_WIDE(7), RT_WIDE(8), RT_WIDE(9)};
 #undef RT_KFN
 #undef RT_SHAPES

@@ -1260,6 +1260,9 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     }
     ds.n_spheres = static_cast<int32_t>(sph.size());
     ds.n_boxes = static_cast<int32_t>(boxes.size());
+    ds.room = boxes.size() == 1 && boxes[0].translate_only;
+    for (int j = 0; j < n_lights && ds.room; ++j)
+        if (lrec[j].dead == 0.0f && (j >= 32 || !((boxes[0].light_inside >> j) & 1u))) ds.room = 0;
     ds.n_mats = n_mats;
     ds.n_lights = n_lights;
     blob.assign(static_cast<size_t>(off > 0 ? off : 1), float4{0, 0, 0, 0});

@@ -497,14 +497,21 @@ def test_origin_lists_change_nothing(gpu_ctx, n_spheres, seed, depth, w, h):
 
 @pytest.mark.parametrize("n_spheres,n_boxes,seed,w,h", [(16, 1, 0, 1920, 1080), (4, 1, 2, 320, 180),
                                                          (32, 1, 5, 320, 180), (64, 1, 1, 320, 180),
-                                                         (16, 3, 3, 320, 180), (48, 2, 4, 256, 144)])
+                                                         (16, 3, 3, 320, 180), (48, 2, 4, 256, 144),
+                                                         (16, 0, 6, 320, 180), (24, -1, 7, 320, 180)])
 def test_scene_shapes_change_nothing(gpu_ctx, n_spheres, n_boxes, seed, w, h):
     """RT_OPT_SCENE_SHAPES (depth-0 renders of LDS-mask scenes run a kernel
-    compiled for the scene's mask width and box count, rt_internal.h
-    kShapeOneBox) gives bit-identical frames against the general kernel and
-    the oracle, for 2-, 4- and 8-byte masks, one box and several, as single
-    frames, a device-buffer batch and Monte-Carlo sums."""
+    compiled for the scene's mask width and for a room — one translate-only
+    box holding every live light, rt_internal.h kShapeRoom) gives
+    bit-identical frames against the general kernel and the oracle, for 2-,
+    4- and 8-byte masks, the room, several boxes, no box and one box that is
+    not a room (n_boxes -1: the room replaced by a small rotated box), as
+    single frames, a device-buffer batch and Monte-Carlo sums."""
     objs = scenes.bench_objects(n_spheres, seed=seed)
+    if n_boxes <= 0:  # no room: no box at all, or one small rotated box the lights are outside of
+        objs = objs[1:]
+        if n_boxes < 0:
+            objs.append(scenes.box((-1.0, -0.5, -0.5), (1.0, 0.5, 0.5), (0.0, 0.0, -6.0), (20.0, 35.0, 0.0), 3))
     for k in range(1, n_boxes):  # more boxes: small rotated cubes among the spheres
         objs.append(scenes.box((-0.5, -0.5, -0.5), (0.5, 0.5, 0.5), (2.0 * k - 3.0, -4.0, 1.5 * k),
                                (0.0, 30.0 * k, 0.0), k % 7))
@@ -534,14 +541,17 @@ def test_scene_shapes_change_nothing(gpu_ctx, n_spheres, n_boxes, seed, w, h):
 
 @pytest.mark.parametrize("n_spheres,n_boxes,seed,depth,w,h", [(64, 1, 0, 2, 480, 270), (256, 1, 1, 4, 320, 180),
                                                                (100, 2, 2, 3, 320, 180), (33, 1, 3, 9, 160, 90),
-                                                               (200, 3, 4, 5, 256, 144)])
+                                                               (200, 3, 4, 5, 256, 144), (64, -1, 5, 3, 320, 180)])
 def test_wide_scene_shapes_change_nothing(gpu_ctx, n_spheres, n_boxes, seed, depth, w, h):
     """RT_OPT_SCENE_SHAPES for the recursive kernels (scenes whose shadow
     queries walk the wide masks' candidate lists and whose secondary rays the
-    origin-sphere lists take, one box or several, rt_internal.h kShapeWide):
-    bit-identical frames against the general kernel and the oracle, single
-    frames and a batch of views in one queued launch."""
+    origin-sphere lists take, the room or several boxes or one box that is not
+    a room, rt_internal.h kShapeWide, kShapeRoom): bit-identical frames
+    against the general kernel and the oracle, single frames and a batch of
+    views in one queued launch."""
     objs = scenes.bench_objects(n_spheres, seed=seed)
+    if n_boxes < 0:  # the room replaced by one small rotated box the lights are outside of
+        objs = objs[1:] + [scenes.box((-1.0, -0.5, -0.5), (1.0, 0.5, 0.5), (0.0, 0.0, -6.0), (20.0, 35.0, 0.0), 3)]
     for k in range(1, n_boxes):
         objs.append(scenes.box((-0.5, -0.5, -0.5), (0.5, 0.5, 0.5), (2.0 * k - 3.0, -4.0, 1.5 * k),
                                (0.0, 30.0 * k, 0.0), k % 7))

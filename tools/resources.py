@@ -42,7 +42,7 @@ def lib_path(spec):
 
 def kernel_name(mangled):
     """render_kernel<D, MC, DEV[, SHAPE]> from the mangled name (SHAPE: the
-    depth-0 scene shapes, rt_internal.h kShapeOneBox), else the mangled name."""
+    scene shapes, rt_internal.h kShapeRoom), else the mangled name."""
     m = re.search(r"render_kernelILi(\d)ELb([01])ELb([01])E(?:Li(\d+)E)?", mangled)
     if m:
         name = "render_kernel<%s,%s,%s" % (m.group(1), "true" if m.group(2) == "1" else "false",
