@@ -788,25 +788,25 @@ __device__ __forceinline__ Hit closest(const Scene &S, const Ray &r, bool valid,
 }
 
 // Mask of the texel of direction u in a light's cube map (rt_internal.h,
-// kMaskMaxSpheres): face = the largest |component| (ties to the lower axis),
-// column / row from the other two components over it. Approximate
+// kMaskMaxSpheres): face = the largest |component| (ties to z, then y), column
+// / row from the hardware's face coordinates over it. Approximate
 // arithmetic: the host's texel cones carry a margin far above its error. A
 // direction without a usable largest component gets every sphere.
 // Texel of direction u, or -1.
 __device__ __forceinline__ int direction_texel(int n, v3 u) {
-    const float ax = fabsf(u.x), ay = fabsf(u.y), az = fabsf(u.z);
-    const bool fx = ax >= ay && ax >= az, fy = !fx && ay >= az;
-    const float um = fx ? u.x : (fy ? u.y : u.z);
-    const float ua = fx ? u.y : u.x, ub = fy || fx ? u.z : u.y;
-    const int face = 2 * (fx ? 0 : (fy ? 1 : 2)) + (um < 0.0f ? 1 : 0);
-    const float am = fabsf(um);
+    // the cube-map instructions: face id (+x, -x, +y, -y, +z, -z; z, then y
+    // wins a tie), the face coordinates sc, tc and twice the major component
+    // (rt_scene.cpp mask_cones lays the texels out in the same coordinates)
+    const float face = __builtin_amdgcn_cubeid(u.x, u.y, u.z);
+    const float sc = __builtin_amdgcn_cubesc(u.x, u.y, u.z), tc = __builtin_amdgcn_cubetc(u.x, u.y, u.z);
+    const float ma = fabsf(__builtin_amdgcn_cubema(u.x, u.y, u.z));  // 2 |major|
     // (computed in every lane and selected instead of the early return:
     // measured even, r02k)
-    if (!(am > 1e-20f && am < 1e30f)) return -1;
-    const float h = 0.5f * static_cast<float>(n) * __builtin_amdgcn_rcpf(am);
-    const int col = min(max(static_cast<int>(floorf(ua * h + 0.5f * n)), 0), n - 1);
-    const int row = min(max(static_cast<int>(floorf(ub * h + 0.5f * n)), 0), n - 1);
-    return (face * n + row) * n + col;
+    if (!(ma > 2e-20f && ma < 2e30f)) return -1;
+    const float h = static_cast<float>(n) * __builtin_amdgcn_rcpf(ma);
+    const int col = min(max(static_cast<int>(floorf(sc * h + 0.5f * n)), 0), n - 1);
+    const int row = min(max(static_cast<int>(floorf(tc * h + 0.5f * n)), 0), n - 1);
+    return (static_cast<int>(face) * n + row) * n + col;
 }
 __device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int bytes, v3 u, int ns) {
     const int at = direction_texel(n, u);

@@ -680,21 +680,28 @@ const MaskCones &mask_cones(int n) {
     mc->sa.resize(texels);
     std::vector<double> alpha(texels);
     for (int f = 0; f < 6; ++f) {
-        const int m = f >> 1, a = m == 0 ? 1 : 0, b = m == 2 ? 1 : 2;
-        const double sg = (f & 1) ? -1.0 : 1.0;
+        // face f's point (a, b) in the kernel's cube-map coordinates
+        // (direction_texel: the cube instructions' sc / |major|, tc / |major|,
+        // column from sc, row from tc), as a direction
+        auto face_dir = [f](double a, double b, double q[3]) {
+            switch (f) {
+                case 0: q[0] = 1.0; q[1] = -b; q[2] = -a; break;   // +x: sc = -z, tc = -y
+                case 1: q[0] = -1.0; q[1] = -b; q[2] = a; break;   // -x: sc = z, tc = -y
+                case 2: q[0] = a; q[1] = 1.0; q[2] = b; break;     // +y: sc = x, tc = z
+                case 3: q[0] = a; q[1] = -1.0; q[2] = -b; break;   // -y: sc = x, tc = -z
+                case 4: q[0] = a; q[1] = -b; q[2] = 1.0; break;    // +z: sc = x, tc = -y
+                default: q[0] = -a; q[1] = -b; q[2] = -1.0; break; // -z: sc = -x, tc = -y
+            }
+        };
         // a square [a0, a1] x [b0, b1] of the face: its centre direction and
         // the half-angle of the cone through its corners
         auto cone = [&](double a0, double a1, double b0, double b1, double w[3]) {
-            w[m] = sg;
-            w[a] = 0.5 * (a0 + a1);
-            w[b] = 0.5 * (b0 + b1);
+            face_dir(0.5 * (a0 + a1), 0.5 * (b0 + b1), w);
             unit(w);
             double al = 0.0;
             for (int k = 0; k < 4; ++k) {
                 double q[3];
-                q[m] = sg;
-                q[a] = (k & 1) ? a1 : a0;
-                q[b] = (k & 2) ? b1 : b0;
+                face_dir((k & 1) ? a1 : a0, (k & 2) ? b1 : b0, q);
                 unit(q);
                 al = std::max(al, angle(w, q));
             }

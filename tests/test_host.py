@@ -394,23 +394,27 @@ def _scene_blob(objs):
     return buf, meta
 
 
+def _cube_face(u):
+    """The cube-map instructions the kernel's direction_texel uses
+    (v_cubeid / v_cubesc / v_cubetc / v_cubema): face, sc, tc, |major|."""
+    x, y, z = u
+    if abs(z) >= abs(x) and abs(z) >= abs(y):
+        return 4 + (z < 0), (-x if z < 0 else x), -y, abs(z)
+    if abs(y) >= abs(x):
+        return 2 + (y < 0), x, (-z if y < 0 else z), abs(y)
+    return 0 + (x < 0), (z if x < 0 else -z), -y, abs(x)
+
+
 def _direction_texel(n, u):
     """rt_kernel.hip direction_texel in float32 (the approximate reciprocal
     replaced by a division: the lists' margins cover either)."""
     u = np.asarray(u, np.float32)
-    ax_, ay, az = np.abs(u)
-    fx = ax_ >= ay and ax_ >= az
-    fy = (not fx) and ay >= az
-    um = u[0] if fx else (u[1] if fy else u[2])
-    ua = u[1] if fx else u[0]
-    ub = u[2] if (fy or fx) else u[1]
-    face = 2 * (0 if fx else (1 if fy else 2)) + (1 if um < 0 else 0)
-    am = abs(um)
+    face, sc, tc, am = _cube_face(u)
     if not (1e-20 < am < 1e30):
         return -1
     h = np.float32(0.5 * n) / np.float32(am)
-    col = min(max(int(np.floor(ua * h + np.float32(0.5 * n))), 0), n - 1)
-    row = min(max(int(np.floor(ub * h + np.float32(0.5 * n))), 0), n - 1)
+    col = min(max(int(np.floor(sc * h + np.float32(0.5 * n))), 0), n - 1)
+    row = min(max(int(np.floor(tc * h + np.float32(0.5 * n))), 0), n - 1)
     return (face * n + row) * n + col
 
 

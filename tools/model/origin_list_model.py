@@ -38,32 +38,26 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import bvh_model as bm  # noqa: E402
 import walk_model as wm  # noqa: E402
+import shadow_model as sm  # noqa: E402
 
 
 def cube_texels(n):
-    """Per texel of an n x n per-face cube map (face = largest |component|,
-    the kernel's direction_texel layout): unit axis (6 n n, 3) and the
-    half-angle of the cone that holds the texel (axis to its farthest corner)."""
+    """Per texel of an n x n per-face cube map (the kernel's direction_texel
+    layout: the cube-map instructions' face and sc / tc coordinates, as
+    rt_scene.cpp mask_cones): unit axis (6 n n, 3) and the half-angle of the
+    cone that holds the texel (axis to its farthest corner)."""
     axes, halves = [], []
     g = (np.arange(n) + 0.5) / n * 2 - 1
     c = np.arange(n + 1) / n * 2 - 1
     for face in range(6):
-        ax, sign = face // 2, (-1.0 if face % 2 else 1.0)
-        other = [i for i in range(3) if i != ax]  # (col axis, row axis) = the two others in order
         for row in range(n):
             for col in range(n):
-                v = np.zeros(3)
-                v[ax] = sign
-                v[other[0]] = g[col]
-                v[other[1]] = g[row]
-                a = v / np.linalg.norm(v)
+                a = np.array(sm.face_dir(face, g[col], g[row]), float)
+                a /= np.linalg.norm(a)
                 best = 0.0
                 for dr in (0, 1):
                     for dc in (0, 1):
-                        q = np.zeros(3)
-                        q[ax] = sign
-                        q[other[0]] = c[col + dc]
-                        q[other[1]] = c[row + dr]
+                        q = np.array(sm.face_dir(face, c[col + dc], c[row + dr]), float)
                         q /= np.linalg.norm(q)
                         best = max(best, np.arccos(np.clip(a @ q, -1, 1)))
                 axes.append(a)
@@ -73,20 +67,7 @@ def cube_texels(n):
 
 def texel_of(d, n):
     """The kernel's direction_texel (rt_kernel.hip) in float64."""
-    a = np.abs(d)
-    fx = a[0] >= a[1] and a[0] >= a[2]
-    fy = (not fx) and a[1] >= a[2]
-    ax = 0 if fx else (1 if fy else 2)
-    um = d[ax]
-    ua = d[1] if fx else d[0]
-    ub = d[2] if (fy or fx) else d[1]
-    face = 2 * ax + (1 if um < 0 else 0)
-    if not (abs(um) > 1e-20 and abs(um) < 1e30):
-        return -1  # (no usable direction: the lane walks the BVH)
-    hh = 0.5 * n / abs(um)
-    col = min(max(int(np.floor(ua * hh + 0.5 * n)), 0), n - 1)
-    row = min(max(int(np.floor(ub * hh + 0.5 * n)), 0), n - 1)
-    return (face * n + row) * n + col
+    return sm.texel(d, n)
 
 
 def build_lists(S, n, margin=1e-3):

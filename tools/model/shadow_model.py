@@ -79,20 +79,30 @@ def scene_lists(n_spheres):
     return sph, glist, lpos, NT
 
 
+def cube_face(u):
+    """The kernel's cube-map instructions (rt_kernel.hip direction_texel):
+    face (+x, -x, +y, -y, +z, -z; z, then y wins a tie), sc, tc, |major|."""
+    x, y, z = u
+    if abs(z) >= abs(x) and abs(z) >= abs(y):
+        return 4 + int(z < 0), (-x if z < 0 else x), -y, abs(z)
+    if abs(y) >= abs(x):
+        return 2 + int(y < 0), x, (-z if y < 0 else z), abs(y)
+    return int(x < 0), (z if x < 0 else -z), -y, abs(x)
+
+
+def face_dir(face, a, b):
+    """Face `face`'s point (a, b) = (sc, tc) / |major| as a direction
+    (rt_scene.cpp mask_cones)."""
+    return [(1.0, -b, -a), (-1.0, -b, a), (a, 1.0, b), (a, -1.0, -b), (a, -b, 1.0), (-a, -b, -1.0)][face]
+
+
 def texel(u, NT=NT):
-    ax, ay, az = np.abs(u)
-    fx = ax >= ay and ax >= az
-    fy = (not fx) and ay >= az
-    um = u[0] if fx else (u[1] if fy else u[2])
-    ua = u[1] if fx else u[0]
-    ub = u[2] if (fy or fx) else u[1]
-    face = 2 * (0 if fx else (1 if fy else 2)) + (1 if um < 0 else 0)
-    am = abs(um)
+    face, sc, tc, am = cube_face(u)
     if not (1e-20 < am < 1e30):
         return -1
     hh = 0.5 * NT / am
-    col = min(max(int(np.floor(ua * hh + 0.5 * NT)), 0), NT - 1)
-    row = min(max(int(np.floor(ub * hh + 0.5 * NT)), 0), NT - 1)
+    col = min(max(int(np.floor(sc * hh + 0.5 * NT)), 0), NT - 1)
+    row = min(max(int(np.floor(tc * hh + 0.5 * NT)), 0), NT - 1)
     return (face * NT + row) * NT + col
 
 
@@ -100,12 +110,7 @@ def texel_dir(t, NT=NT):
     """Unit direction of texel t's centre (the inverse of texel())."""
     face, rem = divmod(t, NT * NT)
     row, col = divmod(rem, NT)
-    axis, neg = divmod(face, 2)
-    um = -1.0 if neg else 1.0
-    ua = (col + 0.5 - 0.5 * NT) / (0.5 * NT)
-    ub = (row + 0.5 - 0.5 * NT) / (0.5 * NT)
-    v = [(um, ua, ub), (ua, um, ub), (ua, ub, um)][axis]
-    v = np.array(v)
+    v = np.array(face_dir(face, (col + 0.5 - 0.5 * NT) / (0.5 * NT), (row + 0.5 - 0.5 * NT) / (0.5 * NT)))
     return v / np.linalg.norm(v)
 
 
