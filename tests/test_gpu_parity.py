@@ -275,6 +275,41 @@ def test_large_animated_batch_of_scenes(gpu_ctx):
             s.close()
 
 
+@pytest.mark.parametrize("n_views", [4, 10])
+def test_batch_of_scenes_with_different_lights(gpu_ctx, n_views):
+    """rt_render_batch_scenes over two scenes of one layout whose lights
+    differ: the reference's (ambient-only light 0, lights 1-2 inside the room)
+    and one with light 0 lit, light 2 ambient-only and light 1 outside the room
+    (so it is not a room: kShapeRoom must not apply to the launch,
+    rt_api.cpp render_batch_impl). Kernel-argument (4 views) and
+    device-buffer (10 views) batches; every frame equal to its single render
+    and the oracle."""
+    w, h = 160, 90
+    objs = scenes.bench_objects(16, seed=3)
+    la = rt.reference_lights()
+    lb = rt.reference_lights()
+    lb[0].diffuse[:] = [0.6, 0.6, 0.6, 1.0]
+    lb[0].specular[:] = [0.6, 0.6, 0.6, 1.0]
+    lb[2].diffuse[:] = [0.0, 0.0, 0.0, 0.0]
+    lb[2].specular[:] = [0.0, 0.0, 0.0, 0.0]
+    lb[1].position[:] = [30.0, 7.0, 2.0]  # outside the room (x beyond 11)
+    sa, sb = rt.Scene(gpu_ctx, objs, lights=la), rt.Scene(gpu_ctx, objs, lights=lb)
+    try:
+        scs = [sa if k % 2 == 0 else sb for k in range(n_views)]
+        views = [rt.make_view(None, 0.2 * k) for k in range(n_views)]
+        out = dev_zeros((n_views, h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch_scenes(gpu_ctx, scs, out.data_ptr(), w, h, 0, views)
+        got = out.cpu().numpy()
+        for k in range(n_views):
+            single = rt.render(gpu_ctx, scs[k], w, h, 0, view=views[k])
+            assert np.array_equal(got[k], single), k
+            o = port.render(objs, w, h, 0, 0.2 * k, rows=(40, 42), lights=la if k % 2 == 0 else lb)
+            assert np.array_equal(got[k][40:42], o), (k, parity_stats(got[k][40:42], o))
+    finally:
+        sa.close()
+        sb.close()
+
+
 def _inside_sphere_camera():
     cam = rt.Camera()
     cam.position[:] = (-3.0, 4.0, 1.2)  # inside config 1's red-glass sphere (centre (-3, 4, 1), r 2)
