@@ -324,12 +324,15 @@ int rt_multi_last_ms(rt_multi *m, float *kernel_ms, float *gather_ms, float *ass
  * that sphere's precomputed list instead of walking the sphere BVH
  * (depth >= 2); 0: every secondary ray walks the BVH. Output is identical. */
 #define RT_OPT_ORIGIN_LISTS 7
-/* RT_OPT_SCENE_SHAPES (default 1): depth-0 renders of a scene whose shadow
- * queries walk LDS direction masks (at most 64 spheres, culling on) run a
- * kernel compiled for that scene's shape (its mask width, and whether it has
- * exactly one box), the way the reference's shader is compiled for its own
- * scene; 0: every depth-0 render runs the general kernel. Output is
- * identical. */
+/* RT_OPT_SCENE_SHAPES (default 1): a render whose scene has one of the
+ * common shapes runs a kernel compiled for that shape, the way the
+ * reference's shader is compiled for its own scene: at depth 0, shadow
+ * queries that walk LDS direction masks (at most 64 spheres, 12-texel masks,
+ * culling on; the mask width as a constant); at depth >= 2 without
+ * Monte-Carlo, wide masks with their candidate lists and origin-sphere lists
+ * (33-256 spheres, culling on); either with or without the room (exactly one
+ * translate-only box holding every live light). 0: every render runs the
+ * general kernel. Output is identical. */
 #define RT_OPT_SCENE_SHAPES 8
 /* (option 6, a tolerance tier that summed the recursion's colours forward
  * instead of mixing them on the way back up, measured even with the exact
