@@ -78,7 +78,17 @@ cpu_baseline = the reference's own shader on Mesa llvmpipe (oracle/_ref) on the
 host cores, median of 3 dispatches, plus a 1-thread sample and the other
 configs' row subsets (oracle/cpu_baseline.py, child process, N=1 only).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config3|config4|config5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2|config3|config4|config5|shipped]
+
+--gpus N > 1 runs under torch.distributed.run (one rank per GPU, as the driver
+launches it) or on its own: with WORLD_SIZE unset, this process starts the N
+ranks itself (launch_ranks) before anything touches the GPU.
+
+shipped (the reference app's own workload, main.cpp:17-19, raytrace_compute.glsl:
+22, :261-321): 1280x720, the shipped scene moving with time, depth 0; a step
+is F = 256 frames of the animated loop, frame k with its own scene, in one
+rt_render_batch_scenes launch; `draw_loop` is the draw() shape with the
+scene update on the host (rt_scene_update + one synchronous render per frame).
 """
 import argparse
 import datetime
@@ -104,6 +114,14 @@ WORKLOADS = {
                     text="config4: 7680x4320, room box + 256 spheres, max_depth 4 (4 bounces + shadow rays)"),
     "config5": dict(width=1920, height=1080, spheres=16, depth=0, spp=1024,
                     text="config5: 1920x1080 x 1024 spp Monte-Carlo, room box + 16 spheres, max_depth 0"),
+    # the reference app's own workload: its window (main.cpp:17-19), its
+    # shipped scene (4 oriented boxes + 1 sphere, moving with `time`,
+    # raytrace_compute.glsl:261-321) and MAX_RAYTRACE_DEPTH 0 (:22); every
+    # frame of the animated loop has its own scene (rt_render_batch_scenes)
+    "shipped": dict(width=1280, height=720, spheres=1, boxes=4, depth=0,
+                    text="shipped: 1280x720, the reference's own animated scene (4 oriented boxes + 1 sphere, "
+                         "every frame its own scene at t = k/60 s), max_depth 0 (main.cpp:17-19, "
+                         "raytrace_compute.glsl:22, :261-321)"),
 }
 BLOCK_ROWS = 8
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
@@ -354,6 +372,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    if args.workload == "shipped" and world > 1:
+        raise SystemExit("--workload shipped is the reference app's one-GPU frame loop (main.cpp:81-86); "
+                         "the multi-GPU shapes are config2-5's")
     device = local % max(1, torch.cuda.device_count())  # (counting devices does not initialise the GPU)
     coll_dev = "cuda"
     if world > 1:
@@ -372,7 +393,14 @@ def main():
     torch.cuda.set_device(device)
 
     ctx = rt.Context(device)
-    scene = rt.Scene(ctx, rt.bench_objects(cfg["spheres"], 0))
+    wl = args.workload
+    F = args.frames or (7 if wl == "config3" else 256)
+    scenes = None  # shipped: frame k's own scene (the reference's objects at t = k/60 s)
+    if wl == "shipped":
+        scenes = [rt.Scene(ctx, rt.reference_objects(frame_time(k))) for k in range(F)]
+        scene = scenes[0]
+    else:
+        scene = rt.Scene(ctx, rt.bench_objects(cfg["spheres"], 0))
     ctx.set_timing(False)  # no per-launch markers of the library's own
     # Streams of our own: renders are launched asynchronously on `render_s`
     # (the C-ABI treats a NULL stream — torch's default stream handle is 0 —
@@ -396,10 +424,8 @@ def main():
     torch.cuda.set_stream(comm_s)
     sh = render_s.cuda_stream
     assert sh, "need a non-default HIP stream"
-    wl = args.workload
     mc = wl == "config5"
-    batched = wl == "config2" or (wl == "config3" and world == 1)
-    F = args.frames or (256 if wl == "config2" else 7)
+    batched = wl in ("config2", "shipped") or (wl == "config3" and world == 1)
     extra = {}
     surfaces = {"rgba32f": (rt.abi.RT_OUTPUT_RGBA32F, 4, torch.float32, "float4"),
                 "rgb32f": (rt.abi.RT_OUTPUT_RGB32F, 3, torch.float32, "packed float3 (alpha 0 dropped)"),
@@ -409,6 +435,15 @@ def main():
         fmt, ch, dt, text = surfaces[name]
         ctx.set_output(fmt)
         return ch, dt, text
+
+    def render_frames(ptr, j, vs, stream, n_shards=1, shard=0):
+        """Frames j, j+1, ... of the step (views vs) in one rt_render_batch
+        call; `shipped`: each frame with its own scene (rt_render_batch_scenes)."""
+        if scenes is not None:
+            rt.render_batch_scenes(ctx, scenes[j:j + len(vs)], ptr, W, H, DEPTH, vs, BLOCK_ROWS, n_shards, shard,
+                                   stream=stream)
+        else:
+            rt.render_batch(ctx, scene, ptr, W, H, DEPTH, vs, BLOCK_ROWS, n_shards, shard, stream=stream)
 
     def batch_plan(mode, surf):
         """config2: F frames per step (per rank for `none`, all_to_all),
@@ -425,8 +460,7 @@ def main():
 
             def render(buf):
                 for j, vs in chunks:
-                    rt.render_batch(ctx, scene, buf.data_ptr() + esize * j * H * W * ch, W, H, DEPTH, vs,
-                                    stream=cur["s"].cuda_stream)
+                    render_frames(buf.data_ptr() + esize * j * H * W * ch, j, vs, cur["s"].cuda_stream)
             # (two streams: an event pair around every step's launches on its
             # stream, so kernel_ms is each launch's own duration, overlap
             # included, as rocprofv3 reports it; the step time is shorter)
@@ -767,13 +801,41 @@ def main():
         got_all = buf.view(dt).reshape(-1, H, W, ch)
         bad = 0
         for k in frames:
-            rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [rt.make_view(None, frame_time(k))])  # synchronous
+            render_frames(one.data_ptr(), k, [rt.make_view(None, frame_time(k))], None)  # synchronous
             diff = got_all[k].view(torch.int32) != one.view(torch.int32)
             bad += int(diff.reshape(H * W, -1).any(-1).sum().item())
         return {"frames_checked": frames, "pixels": len(frames) * H * W, "mismatched_pixels": bad,
                 "bit_exact": bad == 0,
                 "against": "single-frame renders of the same views (one view per launch, the draw() shape), "
                            "compared as bytes"}
+
+    def verify_bands(buf, bands, accumulate=False):
+        """N=1, one frame per step (configs 4 and 5): rows of the last timed
+        step's frame — config 5: of its accumulator, after the 1/spp scaling
+        — against a render of those rows alone (a launch of its own shape: a
+        tiled launch of the band instead of the frame's queued one; the
+        band's pixels accumulated by a call of their own), compared as bytes
+        (raytrace_compute.glsl:404)."""
+        torch.cuda.synchronize()
+        got = buf.view(torch.int32).reshape(H, W, 4)
+        v0 = rt.make_view(None, 0.0)
+        bad = 0
+        for r0, r1 in bands:
+            band = torch.zeros((r1 - r0, W, 4), dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            if accumulate:
+                rt.render_accumulate(ctx, scene, band.data_ptr(), W, H, DEPTH, spp_mine, sample0, seed=0, view=v0,
+                                     rows=(r0, r1))  # synchronous
+                band.mul_(1.0 / spp)
+            else:
+                rt.render_device(ctx, scene, band.data_ptr(), W, H, DEPTH, view=v0, rows=(r0, r1))  # synchronous
+            torch.cuda.synchronize()
+            bad += int((got[r0:r1] != band.view(torch.int32)).any(-1).sum().item())
+        px = sum(r1 - r0 for r0, r1 in bands) * W
+        return {"rows": [list(b) for b in bands], "pixels": px, "mismatched_pixels": bad, "bit_exact": bad == 0,
+                "against": ("the same rows' samples accumulated by a call of their own (rows only), scaled by "
+                            "1/spp" if accumulate else "a render of the same rows alone (rt_render rows, a tiled "
+                            "launch of the band)") + ", compared as bytes"}
 
     view = None
     if batched:
@@ -808,6 +870,14 @@ def main():
         # its own — byte for byte (raytrace_compute.glsl:404)
         last = plan.bufs[(args.steps - 1) % len(plan.bufs) if plan.per_launch else 0]
         verified = verify_n1(last, sorted({0, (F - 1) // 2, F - 1}), surfaces[surf][1], surfaces[surf][2])
+    elif world == 1 and not args.no_verify and not mc:
+        # config 4 (config 3 at N=1 is batched): two 8-row bands of the last timed frame
+        verified = verify_bands(plan.bufs[(args.steps - 1) % len(plan.bufs)],
+                                [(H // 2, H // 2 + BLOCK_ROWS), (3 * H // 4, 3 * H // 4 + BLOCK_ROWS)])
+    elif world == 1 and not args.no_verify and mc:
+        # config 5: two 2-row bands of the last timed step's estimate
+        verified = verify_bands(accum, [(H // 2 - 2, H // 2), (1000 * H // 1080, 1000 * H // 1080 + 2)],
+                                accumulate=True)
     if world > 1 and not args.no_verify and not mc:
         if batched and mode == "gather":
             verified = verify(plan, F, [frame_time(k) for k in range(F)], surfaces[surf][1], surfaces[surf][2])
@@ -846,7 +916,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(render_s)
             for k in range(n1):
-                rt.render_batch(ctx, scene, one.data_ptr(), W, H, DEPTH, [views1[k % F]], stream=sh)
+                render_frames(one.data_ptr(), k % F, [views1[k % F]], sh)
             e1.record(render_s)
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) / n1 * 1e3
@@ -860,8 +930,7 @@ def main():
             e2.record(render_s)
             s2[1].wait_event(e2)
             for k in range(n1):
-                rt.render_batch(ctx, scene, two[k % 2].data_ptr(), W, H, DEPTH, [views1[k % F]],
-                                stream=s2[k % 2].cuda_stream)
+                render_frames(two[k % 2].data_ptr(), k % F, [views1[k % F]], s2[k % 2].cuda_stream)
             render_s.wait_stream(s2[1])
             e3.record(render_s)
             torch.cuda.synchronize()
@@ -869,8 +938,7 @@ def main():
         # both shapes warmed on both streams, then 3 interleaved repeats each
         # (the chip's clock drifts with load): medians and spreads
         for k in range(4):
-            rt.render_batch(ctx, scene, two[k % 2].data_ptr(), W, H, DEPTH, [views1[k % F]],
-                            stream=s2[k % 2].cuda_stream)
+            render_frames(two[k % 2].data_ptr(), k % F, [views1[k % F]], s2[k % 2].cuda_stream)
         torch.cuda.synchronize()
         ones, twos = [], []
         for _ in range(3):
@@ -887,6 +955,42 @@ def main():
                                                          "and two output buffers; median of 3 repeats "
                                                          "interleaved with the one-stream ones"}}
         del two
+    if wl == "shipped" and rank == 0 and not args.no_single_frame:
+        # the reference's draw() as a drop-in caller runs it (main.cpp:210-238,
+        # INTEGRATION.md): per frame, the scene moved to the frame's time on
+        # the host (rt_scene_update: objects, transforms, shadow masks, upload)
+        # and one synchronous render (NULL stream, the glFinish of :238); wall
+        # clock per frame, host work included
+        live = rt.Scene(ctx, rt.reference_objects(0.0))
+        one_d = torch.empty(H * W * 4, dtype=torch.float32, device="cuda")
+        n_d = max(20, args.steps)
+        torch.cuda.synchronize()
+
+        def draw(k):
+            t = frame_time(k)
+            live.update(rt.reference_objects(t))
+            rt.render_batch(ctx, live, one_d.data_ptr(), W, H, DEPTH, [rt.make_view(None, t)])  # synchronous
+        for k in range(3):
+            draw(k)
+        loops, hosts = [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            for k in range(n_d):
+                draw(k)
+            loops.append((time.perf_counter() - t0) / n_d * 1e6)
+            t0 = time.perf_counter()
+            for k in range(n_d):
+                live.update(rt.reference_objects(frame_time(k)))
+            hosts.append((time.perf_counter() - t0) / n_d * 1e6)
+        us = float(np.median(loops))
+        extra["draw_loop"] = {"us_per_frame": round(us, 3), "value": round(W * H / us, 3), "unit": "Mrays/s",
+                              "scene_update_us": round(float(np.median(hosts)), 3),
+                              "repeats_us": [round(v, 3) for v in loops],
+                              "note": "per frame: Scene.update(rt_reference_objects(t)) + one synchronous "
+                                      "render (NULL stream), wall clock, median of 3 repeats; scene_update_us "
+                                      "is the update alone (host build + upload)"}
+        live.close()
+        del one_d
     if world == 1 and not mc and n_streams["n"] == 1 and not args.no_pipelined:
         # the same steps alternating between two render streams and buffers:
         # a launch's last waves overlap the next step's launch (consecutive
@@ -901,7 +1005,7 @@ def main():
                               "note": "consecutive steps on two alternating streams and buffers"}
         n_streams["n"] = 1
         del pp
-    if batched and wl == "config2" and world == 1 and rank == 0 and not args.no_rgba8:
+    if batched and wl in ("config2", "shipped") and world == 1 and rank == 0 and not args.no_rgba8:
         # the same F frames into the GL_RGBA8 surface the row-tiled N>1
         # steps write (main.cpp:223): the same-surface point of the 1..8-GPU
         # curve, with its 4-B and its float4-equivalent roofline
@@ -932,6 +1036,19 @@ def main():
     fpl = plan.px_per_launch // (W * H) if batched and world == 1 else 1
     build = rt.lib().rt_version().decode()
     pmc = pmc_latest(wl, fpl, build) if world == 1 else {}
+    # a launch stores every pixel once: a PMC summary that writes fewer
+    # bytes than the launch stores belongs to another launch shape (round 5's
+    # mixed-shape average), so none of its figures is this launch's
+    stored = plan.px_per_launch * plan.bytes_per_pixel
+    traffic_check = None
+    if pmc.get("write_bytes_per_launch") is not None:
+        traffic_check = {"write_bytes_per_launch": pmc["write_bytes_per_launch"], "stored_bytes_per_launch": stored,
+                         "ok": pmc["write_bytes_per_launch"] >= 0.99 * stored}
+        if not traffic_check["ok"]:
+            sys.stderr.write("bench.py: profiles/pmc_%s_latest.json writes %.4g B per launch, below the %.4g B the "
+                             "launch stores: not this launch shape's counters; traffic and valu left out\n"
+                             % (wl, pmc["write_bytes_per_launch"], stored))
+            pmc = {}
     traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
         cpu = None
@@ -1005,7 +1122,8 @@ def main():
                          "time_basis": ("step time per launch (two overlapping render streams: a launch's own "
                                         "event span includes its neighbour's run)" if overlapped else
                                         "kernel launch duration (HIP events, one render stream)"),
-                         "bytes_per_launch": plan.px_per_launch * plan.bytes_per_pixel,
+                         "bytes_per_launch": stored,
+                         "traffic_check": traffic_check,
                          "valu": valu_bound(pmc, avg_kernel_ms)},
             "timing": {"per_rank": [dict({"rank": r, "kernel_ms": v[0], "collective_ms": v[1], "assembly_ms": v[2],
                                           "pack_ms": v[3]}, **link_rate(v)) for r, v in enumerate(per_rank)],
@@ -1042,7 +1160,8 @@ def main():
                 line["predicted_ms_per_step"] = pred
         line.update(extra)
         print(json.dumps(line), flush=True)
-    scene.close()
+    for sc in scenes or [scene]:
+        sc.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
@@ -1085,5 +1204,73 @@ def guarded(fn):
         os._exit(EXIT_RANK_FAILED)
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None, grace_s=30.0):
+    """`bench.py --gpus N` with no launcher (WORLD_SIZE unset): start N fresh
+    worker processes of this script, one per GPU, with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as torch.distributed.run sets
+    them — before anything touches the GPU (this parent never imports torch
+    and never re-execs itself) — and relay their output (they share this
+    process's stdout and stderr; rank 0 alone prints the JSON line). Returns
+    0 when every rank exits 0, else the first failing rank's exit status
+    (1 for a signal); once a rank has failed, the others (left waiting in a
+    collective for the missing peer) get `grace_s` seconds and are then
+    killed. A SIGTERM to this parent is passed on to the ranks."""
+    import signal
+    script = script or os.path.abspath(__file__)
+    port = free_port()
+    procs = []
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        raise SystemExit(143)
+    old = signal.signal(signal.SIGTERM, stop)
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the host driver's only kind)
+            procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+        rc = [None] * n
+        deadline = None
+        while any(c is None for c in rc):
+            for i, p in enumerate(procs):
+                if rc[i] is None:
+                    rc[i] = p.poll()
+            if deadline is None and any(c not in (None, 0) for c in rc):
+                deadline = time.monotonic() + grace_s
+            if deadline is not None and time.monotonic() > deadline:
+                for i, p in enumerate(procs):
+                    if rc[i] is None:
+                        p.kill()
+                        rc[i] = p.wait()
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:  # (only after an exception here: every rank has exited otherwise)
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        signal.signal(signal.SIGTERM, old)
+    bad = [(r, c) for r, c in enumerate(rc) if c != 0]
+    if bad:
+        sys.stderr.write("bench.py: %d of %d ranks failed (rank, exit status): %s\n" % (len(bad), n, bad))
+        first = bad[0][1]
+        return first if first > 0 else 1
+    return 0
+
+
 if __name__ == "__main__":
+    if "WORLD_SIZE" not in os.environ:
+        _n = parse().gpus
+        if _n > 1:  # no launcher: this process starts the N ranks itself
+            sys.exit(launch_ranks(_n, sys.argv[1:]))
     guarded(main)

@@ -163,7 +163,18 @@ void rt_destroy(rt_context *ctx);
 
 /* Copies and precomputes (transforms, inverse transforms, normal matrices)
  * the scene and uploads it to the context's device. Arrays are host memory
- * and may be freed after the call. n_objs <= RT_MAX_OBJECTS. */
+ * and may be freed after the call. n_objs <= RT_MAX_OBJECTS.
+ * Host cost (make -C openglraytracer_amd/csrc scene-build-time, 8 host
+ * threads): about 2-5 ms up to 256 spheres. A scene of 33-256 spheres also
+ * gets origin-sphere candidate lists for depth >= 2 renders (RT_OPT_ORIGIN_
+ * LISTS; 12.6 MB and about 30 ms at 256 spheres): they are built and
+ * appended to the device copy by the first render that reads them, never by
+ * create or update, and are not kept on the host.
+ * Stream order: create, update and destroy run on the context's stream, a
+ * blocking HIP stream (see rt_render): their uploads and stream-ordered
+ * frees are ordered after work queued earlier on the device's null stream
+ * (torch's default stream), and null-stream work queued later waits for
+ * them; create and update return only after their upload is complete. */
 #define RT_MAX_OBJECTS 1024
 #define RT_MAX_LIGHTS 16
 #define RT_MAX_MATERIALS 256
@@ -179,7 +190,10 @@ void rt_scene_destroy(rt_scene *scene);
 /* Replace the scene's contents in place (an animated frame: the reference
  * recomputes its objects from `time` every frame, raytrace_compute.glsl:
  * 277-307); reallocates only if the new scene is larger. Waits (on the host)
- * for the renders queued that read the scene, on any stream. */
+ * for the renders queued that read the scene, on any stream. The per-frame
+ * host cost is rt_scene_create's build (about 2-5 ms up to 256 spheres, tens
+ * of microseconds for the shipped scene) plus the upload; a deep render of
+ * the new contents rebuilds the origin-sphere lists once. */
 int rt_scene_update(rt_context *ctx, rt_scene *scene, const rt_object *objs, int n_objs, const rt_material *mats,
                     int n_mats, const rt_light *lights, int n_lights);
 

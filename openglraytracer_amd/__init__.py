@@ -229,8 +229,12 @@ class Context:
         _check(lib().rt_context_set(self._h, abi.RT_OPT_ORIGIN_LISTS, 1 if on else 0))
 
     def set_scene_shapes(self, on):
-        """RT_OPT_SCENE_SHAPES: depth-0 renders of LDS-mask scenes run the
-        kernel compiled for the scene's shape (output identical)."""
+        """RT_OPT_SCENE_SHAPES: a render whose scene has a common shape runs
+        the kernel compiled for it (include/rt.h): at depth 0, LDS-mask scenes
+        (the mask width as a constant); at depth >= 2 without Monte-Carlo,
+        scenes with wide masks, their candidate lists and origin-sphere lists;
+        each with or without the room (one translate-only box holding every
+        live light). Output identical either way."""
         _check(lib().rt_context_set(self._h, abi.RT_OPT_SCENE_SHAPES, 1 if on else 0))
 
     def set_output(self, fmt):

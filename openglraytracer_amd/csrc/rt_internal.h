@@ -280,7 +280,8 @@ struct DeviceScene {
     int32_t off_bvh = 0, n_bvh = 0, off_blink = 0, off_cone = 0;
     int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
     int32_t off_gmask = -1, gmask_words = 0, off_glist = -1;
-    int32_t off_olist = -1;
+    int32_t off_olist = -1;   // -1 until the lists are built (ensure_origin_lists)
+    int32_t olist_eligible = 0;  // kOListMinSpheres..256 spheres: depth >= 2 renders get the lists
     int32_t n_spheres = 0, n_boxes = 0, n_mats = 0, n_lights = 0;
     // 1: the one box is a room: translate-only, every live light strictly
     // inside it (the shadow queries' box shortcut always applies; kShapeRoom)
@@ -332,6 +333,13 @@ LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_
                          int width, int height);
 // launch on `stream` with the context's queue slot and kernel-time events
 int launch(rt_context *ctx, LaunchParams &p, int max_depth, hipStream_t stream);
+// Before a render at max_depth: a scene that reads origin-sphere lists at
+// this depth (max_depth >= 2, RT_OPT_ORIGIN_LISTS on, 33-256 spheres) gets
+// them built and appended to its device blob the first time (the region past
+// the blob the earlier renders read; a larger blob is reallocated and the old
+// one freed behind its renders). One host build + synchronous upload per
+// scene contents; RT_OK at once when nothing is needed.
+int ensure_origin_lists(rt_context *ctx, const rt_scene *scene, int max_depth);
 // a render on `stream` reads `scene`'s blob: remember it (an event on that
 // stream) so that rt_scene_destroy / rt_scene_update wait for it
 int note_scene_use(const rt_scene *scene, hipStream_t stream);

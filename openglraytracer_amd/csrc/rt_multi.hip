@@ -212,6 +212,10 @@ int rt_render_multi_view(rt_multi *m, const rt_scene *const *scenes, const rt_vi
     if (!out_is_device && (rc = ensure(&m->frame, &m->frame_cap, static_cast<size_t>(height) * row_bytes,
                                        "hipMalloc(frame)")) != RT_OK)
         return rc;
+    // (every scene's origin-sphere lists, before any device starts: a first
+    // deep render builds them, rt_internal.h)
+    for (int i = 0; i < n; ++i)
+        if ((rc = ensure_origin_lists(m->ctx[i], scenes[i], max_depth)) != RT_OK) return rc;
     // every device renders its row blocks on its context's stream
     for (int i = 0; i < n; ++i) {
         rt_context *c = m->ctx[i];

@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -961,7 +962,9 @@ static void origin_lists_range(const std::vector<SphereRec> &sph, const std::vec
 }
 
 // The lists of all spheres: independent per origin sphere, built on up to 16
-// host threads (256 spheres: about 130 ms of host work on one thread).
+// host threads (256 spheres: about 130 ms of host work on one thread). A
+// thread that cannot be started (std::system_error, e.g. a process thread
+// limit) leaves its range to the calling thread: nothing throws out of here.
 static void build_origin_lists(const std::vector<SphereRec> &sph, const std::vector<SphereMeta> &smeta, int n,
                                std::vector<uint8_t> &out) {
     const size_t ns = sph.size();
@@ -974,16 +977,52 @@ static void build_origin_lists(const std::vector<SphereRec> &sph, const std::vec
         return;
     }
     std::vector<std::thread> pool;
+    pool.reserve(n_thr);
     const size_t per = (ns + n_thr - 1) / n_thr;
+    size_t started = 0;  // [0, started) is covered by the running workers
     for (size_t k = 0; k < n_thr; ++k) {
         const size_t a = k * per, b = std::min(ns, a + per);
-        if (a < b) pool.emplace_back(origin_lists_range, std::cref(sph), std::cref(smeta), n, std::ref(out), a, b);
+        if (a >= b) break;
+        try {
+            pool.emplace_back(origin_lists_range, std::cref(sph), std::cref(smeta), n, std::ref(out), a, b);
+        } catch (const std::system_error &) {
+            break;
+        }
+        started = b;
     }
+    if (started < ns) origin_lists_range(sph, smeta, n, out, started, ns);
     for (std::thread &t : pool) t.join();
 }
 
+// The origin-sphere lists of a built scene, from its host blob (the sphere
+// records the kernel stages): empty unless the scene has
+// kOListMinSpheres..256 spheres (DeviceScene::olist_eligible).
+int build_origin_lists_for(const std::vector<float4> &host, const DeviceScene &ds, std::vector<uint8_t> &olist) {
+    olist.clear();
+    if (!ds.olist_eligible) return RT_OK;
+    const size_t ns = static_cast<size_t>(ds.n_spheres);
+    if (host.size() * sizeof(float4) < (static_cast<size_t>(ds.off_smeta) * 16 + ns * sizeof(SphereMeta)) ||
+        host.size() * sizeof(float4) < (static_cast<size_t>(ds.off_spheres) * 16 + ns * sizeof(SphereRec))) {
+        set_error("origin lists: the scene's host copy is incomplete");
+        return RT_ERR_INVALID;
+    }
+    std::vector<SphereRec> sph(ns);
+    std::vector<SphereMeta> smeta(ns);
+    const char *base = reinterpret_cast<const char *>(host.data());
+    std::memcpy(sph.data(), base + static_cast<size_t>(ds.off_spheres) * 16, ns * sizeof(SphereRec));
+    std::memcpy(smeta.data(), base + static_cast<size_t>(ds.off_smeta) * 16, ns * sizeof(SphereMeta));
+    try {
+        build_origin_lists(sph, smeta, kOListTexels, olist);
+    } catch (const std::bad_alloc &) {
+        olist.clear();
+        set_error("origin lists: out of memory");
+        return RT_ERR_NOMEM;
+    }
+    return RT_OK;
+}
+
 int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
-                int n_lights, std::vector<float4> &blob, DeviceScene &ds) {
+                int n_lights, std::vector<float4> &blob, DeviceScene &ds, bool with_origin_lists) {
     std::vector<SphereRec> sph;
     std::vector<SphereMeta> smeta;
     std::vector<BoxRec> boxes;
@@ -1257,10 +1296,17 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
         off += units(glist.size());
     }
     // The secondary rays' origin-sphere candidate lists (rt_internal.h
-    // kOListSlots), past the staged part like the wide masks.
+    // kOListSlots), past the staged part like the wide masks. Only depth >= 2
+    // renders read them, and they cost tens of ms of host work and up to
+    // 12.6 MB at 256 spheres: a scene is created without them, and the first
+    // render that reads them appends them to the device blob
+    // (ensure_origin_lists, rt_api.cpp; never to the host copy).
+    // with_origin_lists: built here, at the blob's end (the CPU models'
+    // rt_debug_scene_blob).
     std::vector<uint8_t> olist;
     ds.off_olist = -1;
-    if (sph.size() >= static_cast<size_t>(kOListMinSpheres) && sph.size() <= 256) {
+    ds.olist_eligible = sph.size() >= static_cast<size_t>(kOListMinSpheres) && sph.size() <= 256;
+    if (ds.olist_eligible && with_origin_lists) {
         build_origin_lists(sph, smeta, kOListTexels, olist);
         ds.off_olist = off;
         off += units(olist.size());

@@ -89,4 +89,8 @@ CONFIGS = {
     "config3": (lambda: bench_objects(64), 3840, 2160, 2),
     "config4": (lambda: bench_objects(256), 7680, 4320, 4),
     "config5": (lambda: bench_objects(16), 1920, 1080, 0),
+    # the reference app's own workload: its shipped, time-animated scene
+    # (raytrace_compute.glsl:261-321; None = the unmodified shader's objects,
+    # glref.render) at the window size of main.cpp:17-19, MAX_RAYTRACE_DEPTH 0 (:22)
+    "shipped": (lambda: None, 1280, 720, 0),
 }

@@ -240,3 +240,102 @@ def test_config2_one_gpu_line_checks_itself():
     assert 0.97 <= ratio8 <= 1.01, ratio8
     one = line["single_frame"]
     assert len(one["repeats_us"]) == 3 and len(one["two_streams"]["repeats_us"]) == 3
+
+
+STUB_RANK = r'''
+import json, os, sys
+import torch
+import torch.distributed as dist
+dist.init_process_group("gloo")
+t = torch.tensor([float(dist.get_rank() + 1)])
+dist.all_reduce(t)
+if dist.get_rank() == 0:
+    print(json.dumps({"world": dist.get_world_size(), "sum": t.item(), "argv": sys.argv[1:],
+                      "local_rank": int(os.environ["LOCAL_RANK"])}), flush=True)
+dist.destroy_process_group()
+'''
+
+
+def test_self_launch_starts_every_rank(tmp_path, capfd):
+    """bench.py --gpus N with no launcher (the driver's N=1 command shape,
+    `python3 bench.py --gpus N`): launch_ranks starts N processes with
+    torch.distributed.run's environment, and rank 0's line comes through
+    (a stub rank: gloo all-reduce on the CPU)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    stub = tmp_path / "stub_rank.py"
+    stub.write_text(STUB_RANK)
+    assert bench.launch_ranks(3, ["--steps", "2"], script=str(stub)) == 0
+    out = capfd.readouterr().out
+    lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+    assert lines == [{"world": 3, "sum": 6.0, "argv": ["--steps", "2"], "local_rank": 0}]
+
+
+def test_self_launch_fails_when_a_rank_fails():
+    """The same entry through bench.py itself (gloo, CPU: rank 1 dies right
+    after joining the group, before any GPU work): the launcher's exit is
+    nonzero, every rank has ended, and it says which ranks failed."""
+    env = dict(os.environ, RT_BENCH_FAULT="1:init")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--no-cpu-baseline", "--collective-timeout", "60"],
+                       capture_output=True, text=True, timeout=180, env=env, cwd=ROOT)
+    assert r.returncode != 0
+    assert "injected fault at init" in r.stderr
+    assert "rank 0: step failed, aborting the frame" in r.stderr
+    assert "ranks failed" in r.stderr
+
+
+@pytest.mark.gpu
+def test_self_launched_two_ranks_on_one_gpu():
+    """`python3 bench.py --gpus 2` with no launcher on the one-GPU box: the
+    two self-started ranks render config 2's row-tiled frames through the
+    HIP kernel (gloo), and the assembled frames are verified byte for byte."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--no-cpu-baseline", "--steps", "3", "--warmup", "1", "--frames", "4"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["verified"]["bit_exact"]
+
+
+def _bench_line(*args, timeout=300):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.gpu
+def test_shipped_workload_line():
+    """The reference app's own workload (main.cpp:17-19, raytrace_compute.glsl:
+    22, :261-321): 1280x720, the shipped scene at every frame's time, depth
+    0, 256 frames per launch each with its own scene; frames 0, 127, 255
+    byte-identical to single renders; the draw() shape with the host's
+    scene update is reported beside it."""
+    line = _bench_line("--workload", "shipped", "--steps", "3", "--warmup", "1")
+    cfg = line["config"]
+    assert (cfg["width"], cfg["height"], cfg["max_depth"], cfg["frames_per_launch"]) == (1280, 720, 0, 256)
+    assert line["verified"]["bit_exact"] and line["verified"]["frames_checked"] == [0, 127, 255]
+    assert line["roofline"]["bytes_per_launch"] == 256 * 1280 * 720 * 16
+    d = line["draw_loop"]
+    assert d["us_per_frame"] > 0 and d["scene_update_us"] > 0 and len(d["repeats_us"]) == 3
+    assert line["rgba8_surface"]["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["config4", "config5"])
+def test_one_frame_workloads_verify_what_they_time(workload):
+    """Configs 4 and 5 at N=1 check the buffers of their last timed step:
+    two 8-row bands of the 8K frame against renders of those rows alone,
+    two 2-row bands of the Monte-Carlo estimate against the same samples of
+    those rows accumulated by a call of their own (raytrace_compute.glsl:404)."""
+    line = _bench_line("--workload", workload, "--steps", "1", "--warmup", "1", "--no-pipelined")
+    v = line["verified"]
+    assert v["bit_exact"] and v["mismatched_pixels"] == 0 and len(v["rows"]) == 2

@@ -17,7 +17,8 @@
 
 namespace rtamd {
 int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
-                int n_lights, std::vector<float4> &blob, DeviceScene &ds);
+                int n_lights, std::vector<float4> &blob, DeviceScene &ds, bool with_origin_lists);
+int build_origin_lists_for(const std::vector<float4> &host, const DeviceScene &ds, std::vector<uint8_t> &olist);
 }  // namespace rtamd
 
 namespace {
@@ -39,7 +40,7 @@ void parse_and_build(const std::string &text, float t) {
     ++g_parsed;
     std::vector<float4> blob;
     rtamd::DeviceScene ds;
-    if (rtamd::build_scene(objs.data(), no, mats.data(), nm, lights.data(), nl, blob, ds) == RT_OK) {
+    if (rtamd::build_scene(objs.data(), no, mats.data(), nm, lights.data(), nl, blob, ds, true) == RT_OK) {
         ++g_built;
         rt_view view;
         rt_make_view(hc ? &cam : nullptr, t, &view);
@@ -81,7 +82,7 @@ int main(int argc, char **argv) {
         std::vector<float4> blob;
         rtamd::DeviceScene ds;
         if (rtamd::build_scene(ref, RT_REFERENCE_OBJECTS, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS,
-                               blob, ds) != RT_OK)
+                               blob, ds, true) != RT_OK)
             return 1;
         rt_view v;
         rt_make_view(nullptr, t, &v);
@@ -92,7 +93,7 @@ int main(int argc, char **argv) {
         std::vector<float4> blob;
         rtamd::DeviceScene ds;
         if (rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob,
-                               ds) != RT_OK)
+                               ds, true) != RT_OK)
             return 1;
         ++g_built;
     }

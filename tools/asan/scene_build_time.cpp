@@ -13,7 +13,8 @@
 
 namespace rtamd {
 int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int n_mats, const rt_light *lights,
-                int n_lights, std::vector<float4> &blob, DeviceScene &ds);
+                int n_lights, std::vector<float4> &blob, DeviceScene &ds, bool with_origin_lists);
+int build_origin_lists_for(const std::vector<float4> &host, const DeviceScene &ds, std::vector<uint8_t> &olist);
 }
 
 int main() {
@@ -30,7 +31,7 @@ int main() {
             std::vector<float4> blob;
             rtamd::DeviceScene ds;
             const auto t0 = std::chrono::steady_clock::now();
-            rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds);
+            rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds, false);
             ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
             if (rep == 0) {
                 const unsigned char *b = reinterpret_cast<const unsigned char *>(blob.data());
@@ -40,7 +41,7 @@ int main() {
         std::sort(ms.begin(), ms.end());
         std::vector<float4> blob;
         rtamd::DeviceScene ds;
-        rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds);
+        rtamd::build_scene(objs.data(), n + 1, mats, RT_REFERENCE_MATERIALS, lights, RT_REFERENCE_LIGHTS, blob, ds, false);
         if (ds.off_glist >= 0) {  // candidate-list lengths of the wide masks (rt_internal.h kGListMax)
             const unsigned char *g = reinterpret_cast<const unsigned char *>(blob.data()) + 16L * ds.off_glist;
             const long texels = (static_cast<long>(blob.size()) - ds.off_glist);
@@ -60,6 +61,17 @@ int main() {
         std::printf("room + %3d spheres: scene build %.3f ms (median of 7), blob %016llx, LDS %ld B (masks %d B)\n", n,
                     ms[3], static_cast<unsigned long long>(hash), lds,
                     ds.off_dmask >= 0 ? 16 * (ds.blob_units - ds.off_dmask) : 0);
+        if (ds.olist_eligible) {  // the origin-sphere lists, built on a scene's first deep render
+            std::vector<double> ol;
+            std::vector<uint8_t> olist;
+            for (int rep = 0; rep < 3; ++rep) {
+                const auto t0 = std::chrono::steady_clock::now();
+                rtamd::build_origin_lists_for(blob, ds, olist);
+                ol.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+            }
+            std::sort(ol.begin(), ol.end());
+            std::printf("room + %3d spheres: origin lists %.3f ms (median of 3), %zu B\n", n, ol[1], olist.size());
+        }
     }
     return 0;
 }
