@@ -379,6 +379,10 @@ struct Scene {
     // SGPRs (no LDS round trip, no VGPRs) — used where the index is uniform.
     const __attribute__((address_space(4))) BoxRec *cbox;
     const __attribute__((address_space(4))) LightRec *clight;
+#ifdef RT_UNIFORM_MAT
+    const __attribute__((address_space(4))) MatRec *cmat;
+    const __attribute__((address_space(4))) LightMatRec *clm;
+#endif
     int ns, nb, nl, nm, nbvh;
     int cull;
     int room;  // the one box is a room (kShapeRoom): its shadow shortcut always applies
@@ -1175,8 +1179,16 @@ __device__ unsigned long long rt_phase_buf[kPhaseWaves * 16];
 #endif
 
 // ads_phong_lighting (:789-840). Called with all lanes active.
-__device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Collision &c, bool valid) {
+// kUni (RT_UNIFORM_MAT probe, depth 0): every lane with a hit has material
+// `umat`, and the material and light x material records come by scalar
+// loads (SGPRs) instead of per-lane LDS gathers.
+template <bool kUni = false>
+__device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Collision &c, bool valid, int umat = 0) {
+#if defined(RT_UNIFORM_MAT) && !defined(RT_UNIFORM_MAT_LM_ONLY)
+    const MatRec m = kUni ? cload(S.cmat + umat) : S.mat[c.material];
+#else
     const MatRec &m = S.mat[c.material];
+#endif
     float4 dif = make_float4(0.0f, 0.0f, 0.0f, 0.0f), spe = dif;
     const v3 view = normalize_unit(muls(r.dir, -1.0f));  // ray directions are unit vectors up to rounding
     int slot = -1;  // index among the live lights (direction masks)
@@ -1205,7 +1217,11 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
         const v3 nl = muls(ldir, -1.0f);
         const v3 lref = normalize_unit(sub(nl, muls(c.n, 2.0f * -cos_theta)));
         const float cos_phi = dot(view, lref);
+#ifdef RT_UNIFORM_MAT
+        const LightMatRec q = kUni ? cload(S.clm + (umat * S.nl + j)) : S.lm[c.material * S.nl + j];
+#else
         const LightMatRec &q = S.lm[c.material * S.nl + j];
+#endif
         const float kd = gmax(cos_theta, 0.0f);
         // pow(0, s) is +0 for s > 0 (log2 = -inf, exp2 clamps to 2^-127
         // scaled to 0): skip the polynomials when no lane needs them
@@ -1293,6 +1309,14 @@ __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     RT_PHASE(4);
 #ifdef RT_ABLATE_PHONG
     const v3 col = add(c.p, c.n);
+#elif defined(RT_UNIFORM_MAT)
+    // the first hit lane's material; the scalar-record instance when every
+    // hit lane shares it (97 % of config 2's wave tiles)
+    const uint64_t hb = wave_ballot(hit);
+    const int umat = __builtin_amdgcn_readlane(c.material, static_cast<int>(__builtin_ctzll(hb)));
+    v3 col;
+    if (wave_all(!hit || c.material == umat)) col = phong_impl<true>(S, r, c, hit, umat);
+    else col = phong(S, r, c, hit);
 #else
     const v3 col = phong(S, r, c, hit);
 #endif
@@ -1328,6 +1352,8 @@ struct Frames {
     __device__ __forceinline__ void set(int level, const Frame &v) {
         bits = (bits & ~(15u << (4 * level))) | ((static_cast<uint32_t>(v.flags) & 7u) << (4 * level));
     }
+    __device__ __forceinline__ void set_pending(int, const Frame &) {}
+    __device__ __forceinline__ void pending(int, Ray &r) const { r.start = mk(0.0f, 0.0f, 0.0f); r.dir = mk(0.0f, 0.0f, 1.0f); }
 };
 template <int N>
 struct FramesReal {
@@ -1346,9 +1372,35 @@ struct Frames {
                  // renders config 4 in 11.4 instead of 16.6 ms and config 3 in
                  // 0.82 instead of 0.92 ms; the top levels in LDS, in 768-thread
                  // queued groups, measured config 3 -1 %, config 4 +2 %)
+#ifdef RT_SPLIT_FRAMES
+    // (probe) per level the colour and flags (16 B), and the pending
+    // refraction ray (24 B) only for a node whose refraction child waits
+    // behind its reflection child: fewer scratch bytes per push and pop
+    struct Head {
+        v3 col;
+        int flags;
+    };
+    Head h[N];
+    Ray q[N];
+    __device__ __forceinline__ Frame get(int level) const {
+        Frame f;
+        f.col = h[level].col;
+        f.flags = h[level].flags;
+        return f;
+    }
+    __device__ __forceinline__ void set(int level, const Frame &v) { h[level] = Head{v.col, v.flags}; }
+    __device__ __forceinline__ void set_pending(int level, const Frame &v) { q[level] = Ray{v.rs, v.rd}; }
+    __device__ __forceinline__ void pending(int level, Ray &r) const { r = q[level]; }
+#else
     Frame f[N];
     __device__ __forceinline__ Frame get(int level) const { return f[level]; }
     __device__ __forceinline__ void set(int level, const Frame &v) { f[level] = v; }
+    __device__ __forceinline__ void set_pending(int, const Frame &) {}  // (set stores the whole frame)
+    __device__ __forceinline__ void pending(int level, Ray &r) const {
+        r.start = f[level].rs;
+        r.dir = f[level].rd;
+    }
+#endif
 };
 
 // `emit(value)` receives each lane's colour when its tree is finished (the
@@ -1401,6 +1453,9 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
             const int here = h.slot >= 0 ? h.slot : -1;
             fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3) | (kDepth >= 2 ? (here + 1) << 11 : 0);
             F.set(level, fr);
+#ifdef RT_SPLIT_FRAMES
+            if (sr && st) F.set_pending(level, fr);  // (read back when the refraction child starts)
+#endif
             if (sr) {
                 ray.start = add(c.p, muls(c.n, 0.001f));
                 ray.dir = reflect(ray.dir, c.n);
@@ -1423,8 +1478,12 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
                 if (fr.flags & 1) {  // the refraction child comes next
                     fr.flags = (fr.flags & ~7) | 4;
                     F.set((lv & 0xFF) - 1, fr);
+#ifdef RT_SPLIT_FRAMES
+                    F.pending((lv & 0xFF) - 1, ray);
+#else
                     ray.start = fr.rs;
                     ray.dir = fr.rd;
+#endif
                     if constexpr (kDepth >= 2) lv = (lv & 0xFF) | ((fr.flags >> 11) << 8);
                     next_child = true;
                 } else {
@@ -1875,6 +1934,10 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.olist = kDepth >= 2 && p.off_olist >= 0 ? reinterpret_cast<const uint4 *>(blob + p.off_olist) : nullptr;
     S.cbox = (const __attribute__((address_space(4))) BoxRec *)(blob + p.off_boxes);
     S.clight = (const __attribute__((address_space(4))) LightRec *)(blob + p.off_lights);
+#ifdef RT_UNIFORM_MAT
+    S.cmat = (const __attribute__((address_space(4))) MatRec *)(blob + p.off_mats);
+    S.clm = (const __attribute__((address_space(4))) LightMatRec *)(blob + p.off_lightmat);
+#endif
     S.nbvh = p.n_bvh;
     S.ns = p.n_spheres;
     S.nb = p.n_boxes;

@@ -291,6 +291,15 @@ def main():
     per_tile["lane_utilisation"] = round(tot["rays"] / (64 * tot["iters"]), 4)
     per_tile["ex_bytes_per_pixel"] = round(40 * (tot["ex_store_lanes"] + tot["ex_load_lanes"]) / (64 * a.tiles), 1)
     per_tile["lin_bytes_per_pixel"] = round(28 * (tot["lin_store_lanes"] + tot["lin_load_lanes"]) / (64 * a.tiles), 1)
+    # split frames (round 6, RT_SPLIT_FRAMES): colour + flags (16 B) per push,
+    # fold load and re-store; the pending refraction ray (24 B) stored only by
+    # a node with both children and loaded when its refraction child starts
+    # (the linear scheme's pending-ray counts)
+    per_tile["split_bytes_per_pixel"] = round((16 * (tot["ex_store_lanes"] + tot["ex_load_lanes"]) +
+                                               24 * (tot["lin_store_lanes"] + tot["lin_load_lanes"])) / (64 * a.tiles), 1)
+    per_tile["ex_store_bytes_per_pixel"] = round(40 * tot["ex_store_lanes"] / (64 * a.tiles), 1)
+    per_tile["split_store_bytes_per_pixel"] = round((16 * tot["ex_store_lanes"] + 24 * tot["lin_store_lanes"]) /
+                                                    (64 * a.tiles), 1)
     print(json.dumps({"config": a.config, "tiles": a.tiles, "per_wave_tile": per_tile}))
 
 
