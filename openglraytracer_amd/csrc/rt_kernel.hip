@@ -481,6 +481,32 @@ __device__ __forceinline__ float box_t(const BoxRec &b, v3 rs, v3 rd, bool insid
     bnd = sel(leaving, sl.t2, sl.t1);
     return slab_t(sl);
 }
+// Conservative slab pre-test of a box (local ray rs, rd): false only when the
+// exact slab test (slab(): six correctly rounded quotients q = fl(n / d) of
+// the same numerators n = fl(mins - rs), fl(maxs - rs)) provably misses —
+// t_near >= t_far, t_far <= 0 — or provably gives t_near > t_max >= 0.
+// Here q' = fl(n * v_rcp(d)): v_rcp is within 1 ulp, so |q' - q| <= 2^-21 |q|
+// for |d| >= 2^-60 and finite operands; min and max are monotone, so t_near'
+// and t_far' keep that relative bound, and the decisions below carry a margin
+// of 2^-19 of the magnitudes (4x the bound, the subtraction's rounding
+// included). Anything else — a tiny or non-finite direction component, a
+// non-finite distance — is "may hit", and the exact test decides. So a culled
+// lane is one whose exact test misses: bit-identical results.
+__device__ __forceinline__ bool slab_may_hit(const BoxRec &b, v3 rs, v3 rd, float t_max) {
+    const bool ok = fabsf(rd.x) >= 0x1p-60f && fabsf(rd.y) >= 0x1p-60f && fabsf(rd.z) >= 0x1p-60f;
+    const float ix = __builtin_amdgcn_rcpf(rd.x), iy = __builtin_amdgcn_rcpf(rd.y), iz = __builtin_amdgcn_rcpf(rd.z);
+    const float ax = (b.mins[0] - rs.x) * ix, bx = (b.maxs[0] - rs.x) * ix;
+    const float ay = (b.mins[1] - rs.y) * iy, by = (b.maxs[1] - rs.y) * iy;
+    const float az = (b.mins[2] - rs.z) * iz, bz = (b.maxs[2] - rs.z) * iz;
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    const float an = fabsf(tn), af = fabsf(tf);
+    const bool finite = an < 1e30f && af < 1e30f;  // (NaN fails)
+    const float m = 0x1p-19f;
+    const bool miss = (tn - tf > m * (an + af)) | (tf < -m * af) | (tn > t_max + m * an);
+    return !(ok & finite & miss);
+}
+
 // fl(num / d) < 1 for a non-negative quotient, dividing only when |num| is
 // within 2^-16 of |d| (correctly rounded division is monotonic).
 __device__ __forceinline__ bool quotient_below_one(float num, float d) {
@@ -494,7 +520,9 @@ __device__ __forceinline__ bool quotient_below_one(float num, float d) {
 // Does the box hold an occluder with 0 < t < 1 (:813-816)? light_bit: the
 // light is inside the box with a margin (host, float64), so a segment that
 // starts inside ends inside too and exits past t = 1.
-__device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, uint32_t light_bit, bool room) {
+// pretest: slab_may_hit first (RT_OPT_CULLING; never for the room)
+__device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, uint32_t light_bit, bool room,
+                                             bool pretest) {
     if (room || ((b.light_inside & light_bit) && b.translate_only)) {
         // identity rotation: xform_point is ((1 x + 0 y) + 0 z) + w, which for
         // finite start equals x + w up to the sign of a zero (comparisons
@@ -512,6 +540,14 @@ __device__ __forceinline__ bool box_occludes(const BoxRec &b, v3 start, v3 dir, 
         return quotient_below_one(exit_num(b.mins[0], b.maxs[0], rs.x, rd.x), rd.x) ||
                quotient_below_one(exit_num(b.mins[1], b.maxs[1], rs.y, rd.y), rd.y) ||
                quotient_below_one(exit_num(b.mins[2], b.maxs[2], rs.z, rd.z), rd.z);
+    }
+    if (pretest && !room) {
+        // the exact slab test (six divisions) only where the pre-test
+        // cannot rule out an occluder with 0 < t < 1 (round 6: the shipped
+        // scene's rotated boxes)
+        const bool may = slab_may_hit(b, rs, rd, 1.0f);
+        if (!wave_any(may)) return false;
+        if (!may) return false;
     }
     const float t = slab_t(slab(b, rs, rd));
     return t > 0.0f && t < 1.0f;
@@ -665,7 +701,19 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
         }
         v3 bnd;
         bool leaving;
-        const float t = box_t(B, rs, box_dir(B, r.dir), inside, bnd, leaving);
+        const v3 rd = box_dir(B, r.dir);
+        if (!S.room && S.cull) {
+            // boxes the ray may enter from outside: the exact slab test only
+            // for lanes whose pre-test cannot rule the box out (a ruled-out
+            // lane's exact t is a miss: slab_may_hit), and not at all in a wave
+            // where none can (round 6: the shipped scene's rotated boxes)
+            const bool may = valid && (inside || slab_may_hit(B, rs, rd, 1e30f));
+            if (!wave_any(may)) continue;
+            const float t = box_t(B, rs, rd, inside, bnd, leaving);
+            if (may && closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, (leaving ? 1 : 0) | (box_face(t, bnd) << 1)};
+            continue;
+        }
+        const float t = box_t(B, rs, rd, inside, bnd, leaving);
         if (closer(t, B.obj_index, h)) h = {t, B.obj_index, ~b, (leaving ? 1 : 0) | (box_face(t, bnd) << 1)};
     }
     const v3 d2 = muls(r.dir, 2.0f);
@@ -838,7 +886,7 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
     for (int b = 0; b < S.nb; ++b) {
         // every lane tests (no divergent branch around the test; lanes
         // without the query or already shadowed keep their flag)
-        const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit, S.room != 0);
+        const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit, S.room != 0, S.cull != 0);
         hit = hit | (need & occ);
     }
     if (!wave_any(need && !hit)) return hit;
@@ -1294,10 +1342,10 @@ __device__ __forceinline__ v3 phong(const Scene &S, const Ray &r, const Collisio
 // Depth 0 is one ray (trace0). Deeper trees run as an explicit depth-first
 // walk (trace_tree): every loop iteration traces ONE ray per lane — all lanes
 // execute the same closest-hit + shading code whatever their position in
-// their own tree — with per-level frames (partial colour, pending refraction
-// ray, weights) indexed by the lane's own level, which the compiler keeps in
-// scratch (40 B per level). Lanes whose tree is finished ride along with
-// valid = false.
+// their own tree — with per-level frames (partial colour and flags, 16 B; the
+// pending refraction ray, 24 B, only where both children exist) indexed by
+// the lane's own level, which the compiler keeps in scratch (Frames). Lanes
+// whose tree is finished ride along with valid = false.
 __device__ __forceinline__ v3 trace0(const Scene &S, const Ray &r, bool valid) {
     const v3 black = mk(0.0f, 0.0f, 0.0f);
     RT_PHASE(2);
@@ -1360,22 +1408,22 @@ struct FramesReal {
 #else
 template <int N>
 struct Frames {
-#endif  // per-level frames, indexed by a per-lane level: the compiler keeps them in
-                 // scratch; indexed directly, a push or pop moves one 40-B frame (per-level
-                 // selects read every level's frame: config 4 18.80 vs 19.08 ms, depth-4
-                 // scratch 292 vs 400 B per lane; frames split into colour + flags and
-                 // a pending ray stored only when a refraction child waits measured
-                 // slower, config 4 16.93 -> 17.12 ms, config 3 0.933 -> 0.957 ms, and
-                 // so did field-by-field access of these 40-B frames, config 4
-                 // 16.62 -> 16.91 ms, config 3 0.921 -> 0.948 ms. What the frames
-                 // cost at most: RT_ABLATE_FRAMES, which keeps only the flags,
-                 // renders config 4 in 11.4 instead of 16.6 ms and config 3 in
-                 // 0.82 instead of 0.92 ms; the top levels in LDS, in 768-thread
-                 // queued groups, measured config 3 -1 %, config 4 +2 %)
-#ifdef RT_SPLIT_FRAMES
-    // (probe) per level the colour and flags (16 B), and the pending
-    // refraction ray (24 B) only for a node whose refraction child waits
-    // behind its reflection child: fewer scratch bytes per push and pop
+#endif
+    // Per-level frames, indexed by the lane's level (the compiler keeps them in
+    // scratch): the colour and flags (16 B) of every node with children, and
+    // the pending refraction ray (24 B) only for a node whose refraction child
+    // waits behind its reflection child, read back when that child starts.
+    // Round 6: against one 40-B frame per level (a push storing, a pop loading
+    // all of it), config 4 10.59 -> 10.32 ms, config 3 0.701 -> 0.692 ms, 7
+    // views 0.660 -> 0.643 ms per frame, bit-identical (profiles/r06b_ab.log);
+    // walk_model: 888 -> 521 frame bytes per config-4 pixel. (Round 2 had
+    // measured this split slower, config 4 16.93 -> 17.12 ms, on a walk with
+    // per-level select chains.) Earlier: per-level selects read every level's
+    // frame (config 4 18.80 vs 19.08 ms, depth-4 scratch 292 vs 400 B per
+    // lane); what the frames cost at most: RT_ABLATE_FRAMES, which keeps only
+    // the flags, rendered config 4 in 11.4 instead of 16.6 ms (round 2); the top
+    // levels in LDS, in 768-thread queued groups, measured config 3 -1 %,
+    // config 4 +2 %.
     struct Head {
         v3 col;
         int flags;
@@ -1391,16 +1439,6 @@ struct Frames {
     __device__ __forceinline__ void set(int level, const Frame &v) { h[level] = Head{v.col, v.flags}; }
     __device__ __forceinline__ void set_pending(int level, const Frame &v) { q[level] = Ray{v.rs, v.rd}; }
     __device__ __forceinline__ void pending(int level, Ray &r) const { r = q[level]; }
-#else
-    Frame f[N];
-    __device__ __forceinline__ Frame get(int level) const { return f[level]; }
-    __device__ __forceinline__ void set(int level, const Frame &v) { f[level] = v; }
-    __device__ __forceinline__ void set_pending(int, const Frame &) {}  // (set stores the whole frame)
-    __device__ __forceinline__ void pending(int level, Ray &r) const {
-        r.start = f[level].rs;
-        r.dir = f[level].rd;
-    }
-#endif
 };
 
 // `emit(value)` receives each lane's colour when its tree is finished (the
@@ -1453,9 +1491,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
             const int here = h.slot >= 0 ? h.slot : -1;
             fr.flags = (st ? 1 : 0) | (sr ? 2 : 4) | (c.material << 3) | (kDepth >= 2 ? (here + 1) << 11 : 0);
             F.set(level, fr);
-#ifdef RT_SPLIT_FRAMES
             if (sr && st) F.set_pending(level, fr);  // (read back when the refraction child starts)
-#endif
             if (sr) {
                 ray.start = add(c.p, muls(c.n, 0.001f));
                 ray.dir = reflect(ray.dir, c.n);
@@ -1478,12 +1514,7 @@ __device__ __forceinline__ void trace_tree(const Scene &S, Ray ray, bool active,
                 if (fr.flags & 1) {  // the refraction child comes next
                     fr.flags = (fr.flags & ~7) | 4;
                     F.set((lv & 0xFF) - 1, fr);
-#ifdef RT_SPLIT_FRAMES
                     F.pending((lv & 0xFF) - 1, ray);
-#else
-                    ray.start = fr.rs;
-                    ray.dir = fr.rd;
-#endif
                     if constexpr (kDepth >= 2) lv = (lv & 0xFF) | ((fr.flags >> 11) << 8);
                     next_child = true;
                 } else {

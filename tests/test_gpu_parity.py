@@ -1387,3 +1387,78 @@ def test_random_scenes_batch_shards_rgba8_and_mc(gpu_ctx, seed):
             assert np.array_equal(acc.cpu().numpy(), o, equal_nan=True), (seed, parity_stats(acc.cpu().numpy(), o))
     finally:
         sc.close()
+
+
+def box_scene(seed):
+    """A seeded scene of many oriented boxes (round 6: the slab pre-test,
+    slab_may_hit): the room or not, 4-12 rotated boxes of random extents
+    (thin slabs, long bars, cubes; some around the orbit camera's path, some
+    holding a light), 0-8 spheres, 1-3 lights, the reference materials; the
+    shipped scene's kind of work (raytrace_compute.glsl:261-321) with more of
+    it."""
+    rng = np.random.default_rng(5000 + seed)
+    mats = rt.reference_materials()
+    lights = []
+    for _ in range(int(rng.integers(1, 4))):
+        lt = rt.abi.Light()
+        lt.position[:] = rng.uniform(-8.0, 8.0, 3)
+        lt.ambient[:] = rng.uniform(0.0, 0.2, 4)
+        lt.diffuse[:] = rng.uniform(0.2, 1.0, 4)
+        lt.specular[:] = rng.uniform(0.2, 1.0, 4)
+        lights.append(lt)
+    objs = [scenes.room_box()] if rng.random() < 0.7 else []
+    for _ in range(int(rng.integers(4, 13))):
+        kind = rng.integers(3)
+        ext = (rng.uniform(0.5, 6.0, 3) * np.array([1.0, 1.0, 0.05]) if kind == 0 else
+               rng.uniform(0.1, 0.6, 3) * np.array([1.0, 1.0, 12.0]) if kind == 1 else rng.uniform(0.2, 2.5, 3))
+        objs.append(scenes.box(tuple(-ext), tuple(ext * rng.uniform(0.5, 1.0, 3)), tuple(rng.uniform(-7.0, 7.0, 3)),
+                               tuple(rng.uniform(0.0, 360.0, 3)), int(rng.integers(len(mats)))))
+    for _ in range(int(rng.integers(0, 9))):
+        objs.append(scenes.sphere(tuple(rng.uniform(-7.0, 7.0, 3)), float(rng.uniform(0.2, 1.2)),
+                                  int(rng.integers(len(mats)))))
+    t = float(rng.uniform(0.0, 20.0))
+    return objs, mats, lights, t, int(rng.integers(0, 4)), int(rng.integers(48, 128)), int(rng.integers(32, 80))
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_box_scenes_match_oracle(gpu_ctx, seed):
+    """Many oriented boxes: the conservative slab pre-test (approximate
+    reciprocals, 2^-19 margins) in front of the exact six-division box test,
+    for primary, secondary and shadow rays, leaves every pixel bit-identical
+    to the oracle, with culling on (pre-test) and off (every box tested)."""
+    objs, mats, lights, t, depth, w, h = box_scene(seed)
+    view = rt.make_view(None, t)
+    sc = rt.Scene(gpu_ctx, objs, materials=mats, lights=lights)
+    try:
+        g = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+        gpu_ctx.set_culling(False)
+        off = rt.render(gpu_ctx, sc, w, h, depth, view=view)
+    finally:
+        gpu_ctx.set_culling(True)
+        sc.close()
+    o = oracle_render(objs, w, h, depth, t, materials=mats, lights=lights)
+    desc = (seed, len(objs), len(lights), depth, w, h, round(t, 3))
+    assert np.array_equal(g, o, equal_nan=True), (desc, parity_stats(g, o))
+    assert np.array_equal(off, o, equal_nan=True), (desc, parity_stats(off, o))
+
+
+def test_shipped_scene_animated_batch_full_frames(gpu_ctx):
+    """The shipped workload's launch (bench.py --workload shipped): 1280x720
+    frames of the reference's own animated scene, each view with its own
+    scene in one rt_render_batch_scenes launch, bit-identical to the oracle
+    on bands of rows of three of the frames (t = 0, 2.1, 4.25 s)."""
+    times = [0.0, 2.1, 4.25]
+    w, h = 1280, 720
+    scs = [rt.Scene(gpu_ctx, rt.reference_objects(x)) for x in times]
+    try:
+        out = dev_zeros((len(times), h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch_scenes(gpu_ctx, scs, out.data_ptr(), w, h, 0, [rt.make_view(None, x) for x in times])
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+    finally:
+        for s in scs:
+            s.close()
+    for k, x in enumerate(times):
+        for r0, r1 in [(0, 4), (300, 308), (716, 720)]:
+            o = oracle_render(rt.reference_objects(x), w, h, 0, x, rows=(r0, r1))
+            assert np.array_equal(got[k, r0:r1], o), (x, r0, parity_stats(got[k, r0:r1], o))

@@ -4,7 +4,8 @@
 
 BUILD is a directory under _ab (tools/ablate.sh) or "main" for the
 in-tree library, optionally with context options (main:1=0 = RT_OPT_CULLING
-off). CONFIG is config1..config4, "config2x8" (8 animated frames per launch,
+off). CONFIG is config1..config4, "shipped" (the reference's own scene at
+1280x720, depth 0), "config2x8" (8 animated frames per launch,
 rt_render_batch) or "config5" (Monte-Carlo, 16 jittered samples per launch).
 Every build gets its own context and scene; each round times every build once
 — REPS/2 untimed launches, then one event pair around REPS back-to-back
@@ -86,13 +87,16 @@ for cfg in cfgs:
     build, w, h, depth = scenes.CONFIGS[cfg.split("x")[0]]
     views = (rt.View * max(batch, 1))(*[rt.make_view(None, k / 60.0) for k in range(max(batch, 1))])
     objs = build()
+    if objs is None:  # "shipped": the reference's own scene (at t = 0 for every view)
+        objs = rt.reference_objects(0.0)
     oa = (rt.Object * len(objs))(*objs)
     ma = (rt.Material * len(mats))(*mats)
     la = (rt.Light * len(lights))(*lights)
     out = torch.empty((max(batch, 1), h, w, 4), dtype=torch.float32, device="cuda")
     # sustained timing: each timed block is about 60 ms of GPU work (short
     # bursts run at a higher clock than the bench's back-to-back launches)
-    est_ms = {"config1": 0.03, "config2": 0.045, "config3": 1.0, "config4": 15.0, "config5": 0.045 * 16}.get(
+    est_ms = {"config1": 0.03, "config2": 0.045, "config3": 1.0, "config4": 15.0, "config5": 0.045 * 16,
+              "shipped": 0.045}.get(
         cfg.split("x")[0], 1.0) * max(batch, 1)
     reps = max(2, int(round(60.0 / est_ms)))
     state = {}
