@@ -702,6 +702,9 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
         v3 bnd;
         bool leaving;
         const v3 rd = box_dir(B, r.dir);
+#ifdef RT_ABLATE_BOX_PRIMARY
+        if (kPrimary && !S.room && !inside) continue;  // (timing probe: wrong images by design)
+#endif
         if (!S.room && S.cull) {
             // boxes the ray may enter from outside: the exact slab test only
             // for lanes whose pre-test cannot rule the box out (a ruled-out
@@ -884,6 +887,9 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
     RT_STAT(7, need);
     RT_STAT(10, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
     for (int b = 0; b < S.nb; ++b) {
+#ifdef RT_ABLATE_BOX_SHADOW
+        if (!S.room && b > 0) continue;  // (timing probe: wrong images by design)
+#endif
         // every lane tests (no divergent branch around the test; lanes
         // without the query or already shadowed keep their flag)
         const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit, S.room != 0, S.cull != 0);

@@ -2,6 +2,7 @@
 
     python tools/resources.py [LIB.so | BUILD ...]        (default: the in-tree library)
     python tools/resources.py --gate BASE.so VARIANT.so   exit 1 if VARIANT spills more
+    python tools/resources.py --markdown [BUILD]          DESIGN.md §3's occupancy table
 
 Reads the gfx950 code object out of the library's .hip_fatbin section
 (llvm-objcopy + clang-offload-bundler) and its kernel metadata notes
@@ -106,8 +107,38 @@ def gate(base, variant, kernels=None):
     return bad
 
 
+# DESIGN.md §3's occupancy table: (row label, kernel) in the order it lists them
+TABLE = [
+    ("depth 0, config 2 (room, 2-B masks, > 8 views: device views)", "render_kernel<0,false,true,18>"),
+    ("depth 0, the shipped scene (2-B masks, 4 boxes, device views)", "render_kernel<0,false,true,2>"),
+    ("depth 0, Monte-Carlo, config 5", "render_kernel<0,true,false,18>"),
+    ("depth 0, general", "render_kernel<0,false,false>"),
+    ("depth 0, Monte-Carlo, general", "render_kernel<0,true,false>"),
+    ("depth 1 (config 1)", "render_kernel<1,false,false>"),
+    ("depth 2, config 3 (room, wide masks, origin lists)", "render_kernel<2,false,false,48>"),
+    ("depth 2, general", "render_kernel<2,false,false>"),
+    ("depth 4, config 4 (room, wide masks, origin lists)", "render_kernel<4,false,false,48>"),
+    ("depth 4, general", "render_kernel<4,false,false>"),
+]
+
+
+def markdown(spec="main"):
+    """The occupancy table of DESIGN.md §3, from the library's code object."""
+    res = resources(lib_path(spec))
+    rows = ["| kernel | VGPRs | SGPRs | waves / SIMD | scratch B / lane |", "|---|---|---|---|---|"]
+    for label, k in TABLE:
+        r = res.get(k)
+        if r:
+            rows.append("| %s: `%s` | %d | %d | %d | %d |" % (label, k, r["vgpr"], r["sgpr"], r["waves_per_simd"],
+                                                            r["scratch"]))
+    return "\n".join(rows)
+
+
 def main():
     args = sys.argv[1:]
+    if args[:1] == ["--markdown"]:
+        print(markdown(args[1] if len(args) > 1 else "main"))
+        return
     if args[:1] == ["--gate"]:
         bad = gate(args[1], args[2])
         for k, x, y in bad:
