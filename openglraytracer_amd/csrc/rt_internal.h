@@ -246,6 +246,8 @@ struct LaunchParams {
     // -1: none (last: the depth-0/1 kernels, which never read it, keep their
     // argument layout)
     int32_t off_olist;
+    // 1: the LDS direction masks carry a bit per box (bit n_spheres + b)
+    int32_t dmask_box;
     // host only (the kernels never read it): 1 when every view of the launch
     // culls, so the depth-0 kernels may take the scene's shape (scene_shape)
     int32_t shape_cull;
@@ -279,6 +281,7 @@ struct DeviceScene {
     int32_t off_spheres = 0, off_smeta = 0, off_boxes = 0, off_mats = 0, off_lights = 0, off_lightmat = 0;
     int32_t off_bvh = 0, n_bvh = 0, off_blink = 0, off_cone = 0;
     int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
+    int32_t dmask_box = 0;  // the LDS masks carry a bit per box, bit n_spheres + b (round 6)
     int32_t off_gmask = -1, gmask_words = 0, off_glist = -1;
     int32_t off_olist = -1;   // -1 until the lists are built (ensure_origin_lists)
     int32_t olist_eligible = 0;  // kOListMinSpheres..256 spheres: depth >= 2 renders get the lists

@@ -368,6 +368,7 @@ struct Scene {
     const ShadowCone *cone;  // [light][sphere] shadow culling cones
     const char *dmask;  // [live light][face][row][col] shadow direction masks (nullptr: none)
     int dmask_n, dmask_bytes;
+    int dmask_box;  // the masks carry a bit per box (bit ns + b)
     const uint64_t *gmask;  // wide masks in global memory: [live light][texel][word] (nullptr: none)
     const uint4 *glist;     // their candidate lists: [live light][texel] (nullptr: none)
     int gwords;
@@ -863,9 +864,10 @@ __device__ __forceinline__ int direction_texel(int n, v3 u) {
     const int row = min(max(static_cast<int>(floorf(tc * h + 0.5f * n)), 0), n - 1);
     return (static_cast<int>(face) * n + row) * n + col;
 }
-__device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int bytes, v3 u, int ns) {
+// (nbits: the mask's sphere and box bits)
+__device__ __forceinline__ uint64_t direction_mask(const void *tab, int n, int bytes, v3 u, int nbits) {
     const int at = direction_texel(n, u);
-    if (at < 0) return ns >= 64 ? ~uint64_t{0} : (uint64_t{1} << ns) - 1u;
+    if (at < 0) return nbits >= 64 ? ~uint64_t{0} : (uint64_t{1} << nbits) - 1u;
     if (bytes == 8) return static_cast<const uint64_t *>(tab)[at];
     return bytes == 2 ? static_cast<const uint16_t *>(tab)[at] : static_cast<const uint32_t *>(tab)[at];
 }
@@ -886,10 +888,22 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
     const uint32_t light_bit = light < 32 ? 1u << light : 0u;
     RT_STAT(7, need);
     RT_STAT(10, (threadIdx.x & 63) == __builtin_ctzll(__ballot(1)));
+    // the LDS masks' box bits (round 6; `mask` is the lane's LDS mask where
+    // there are no wide masks): a lane whose bit of box b is clear cannot be
+    // occluded by it (its bounding sphere's cone from the light, the spheres'
+    // test), and a wave none of whose lanes has the bit skips the box
+    const bool box_bits = S.dmask_box != 0 && S.cull && S.dmask != nullptr && S.gmask == nullptr;
     for (int b = 0; b < S.nb; ++b) {
 #ifdef RT_ABLATE_BOX_SHADOW
         if (!S.room && b > 0) continue;  // (timing probe: wrong images by design)
 #endif
+        if (box_bits) {
+            const bool cand = need && !hit && ((mask >> (S.ns + b)) & 1u) != 0u;
+            if (!wave_any(cand)) continue;
+            const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit, S.room != 0, S.cull != 0);
+            hit = hit | (cand & occ);
+            continue;
+        }
         // every lane tests (no divergent branch around the test; lanes
         // without the query or already shadowed keep their flag)
         const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit, S.room != 0, S.cull != 0);
@@ -900,7 +914,8 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
         // the LDS-mask walk (see below) with the ray's quadratic terms
         // computed only when some lane of the wave has a candidate (most
         // shadow queries of a wave have none: config 2 -1 %)
-        const uint64_t m64 = need && !hit ? mask : 0u;
+        // (the sphere bits: the box bits above them dropped)
+        const uint64_t m64 = (need && !hit ? mask : 0u) & (box_bits ? (uint64_t{1} << (S.ns & 63)) - 1u : ~uint64_t{0});
         if (!wave_any(m64 != 0u)) return hit;
         const v3 d2 = muls(dir, 2.0f);
         const float qa = dot(dir, dir);
@@ -1315,7 +1330,7 @@ __device__ __forceinline__ v3 phong_impl(const Scene &S, const Ray &r, const Col
                 smask = static_cast<uint64_t>(static_cast<int64_t>(direction_texel(kGMaskTexels, muls(sdir, -1.0f))));
             else if (S.dmask && !S.gmask)
                 smask = direction_mask(S.dmask + slot * 6 * S.dmask_n * S.dmask_n * S.dmask_bytes, S.dmask_n,
-                                       S.dmask_bytes, muls(sdir, -1.0f), S.ns);
+                                       S.dmask_bytes, muls(sdir, -1.0f), S.ns + (S.dmask_box ? S.nb : 0));
             const bool shadowed = occluded(S, add(c.p, muls(c.n, 0.01f)), sdir, c.p, lpos, j, slot, smask, need,
                                            S.glist ? &pre : nullptr);
             if (need && !shadowed) {
@@ -1783,6 +1798,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
     if constexpr ((kShape & kShapeRoom) != 0) {
         S.nb = 1;
         S.room = 1;
+        S.dmask_box = 0;  // (a room scene's masks carry no box bits: rt_scene.cpp)
     }
     RT_CYC(kCycRaygen);
     if (!wave_any(px.active)) return;
@@ -1963,6 +1979,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.dmask = p.off_dmask >= 0 ? reinterpret_cast<const char *>(lds + p.off_dmask) : nullptr;
     S.dmask_n = p.dmask_n;
     S.dmask_bytes = p.dmask_bytes;
+    S.dmask_box = p.dmask_box;
     // (recursive depths only: the depth-0/1 kernels keep their register
     // budget and use the per-wave cone for such scenes)
     S.gmask = kDepth >= 2 && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;

@@ -1191,8 +1191,20 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     std::vector<uint64_t> dmask;
     ds.off_dmask = -1;
     ds.dmask_n = 0;
-    if (!sph.empty() && sph.size() <= static_cast<size_t>(kMaskMaxSpheres) && n_live > 0) {
-        ds.dmask_bytes = sph.size() <= 16 ? 2 : (sph.size() <= 32 ? 4 : 8);
+    // Round 6: in a scene of several boxes the boxes get mask bits too (bit
+    // n_spheres + b), from their bounding spheres. A box that can occlude a
+    // shadow segment holds a point of it, and so does its bounding sphere: the
+    // spheres' cone test is conservative for it. The sphere's radius carries
+    // 1e-3 relative + 1e-3 (1 + |centre|) of margin over the float64 half
+    // diagonal, far above the float32 transforms' error. The choice depends
+    // on the object kinds alone (the blob layout rt_render_batch_scenes
+    // requires to be shared by the frames of an animated scene): a one-box
+    // scene — the room of configs 2-5 — keeps its box's shortcuts instead.
+    const bool box_bits = boxes.size() >= 2;
+    const size_t mask_bits = sph.size() + (box_bits ? boxes.size() : 0);
+    ds.dmask_box = 0;
+    if (!sph.empty() && mask_bits <= static_cast<size_t>(kMaskMaxSpheres) && n_live > 0) {
+        ds.dmask_bytes = mask_bits <= 16 ? 2 : (mask_bits <= 32 ? 4 : 8);
 #ifndef RT_DMASK_MAXN
 #define RT_DMASK_MAXN 12
 #endif
@@ -1207,7 +1219,34 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     }
     std::vector<char> dmask_bytes;
     if (ds.dmask_n > 0) {
-        build_direction_masks(sph, smeta, lights, lrec, ds.dmask_n, dmask);
+        if (box_bits) {
+            std::vector<SphereRec> bsph(sph);
+            std::vector<SphereMeta> bmeta(smeta);
+            for (int i = 0; i < n_objs; ++i) {
+                const rt_object &o = objs[i];
+                if (object_kind(o) != 1) continue;
+                const M4 T = transform(o.position, o.angles);
+                double c[3], h2 = 0.0;
+                for (int r = 0; r < 3; ++r) {
+                    const double lc = 0.5 * (double(o.box_mins[r]) + double(o.box_maxs[r]));
+                    const double e = 0.5 * (double(o.box_maxs[r]) - double(o.box_mins[r]));
+                    h2 += e * e;
+                    c[r] = lc;
+                }
+                double w[3];
+                for (int r = 0; r < 3; ++r) w[r] = T.m[0][r] * c[0] + T.m[1][r] * c[1] + T.m[2][r] * c[2] + T.m[3][r];
+                const double wl = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+                const double rad = std::sqrt(h2) * 1.001 + 1e-3 * (1.0 + wl);
+                bsph.push_back({static_cast<float>(w[0]), static_cast<float>(w[1]), static_cast<float>(w[2]), 0.0f});
+                // (a non-finite box: a non-finite radius, the bit set everywhere)
+                bmeta.push_back({i, o.material, std::isfinite(rad) ? static_cast<float>(rad * (1.0 + 1e-6))
+                                                                   : HUGE_VALF, 0});
+            }
+            build_direction_masks(bsph, bmeta, lights, lrec, ds.dmask_n, dmask);
+            ds.dmask_box = 1;
+        } else {
+            build_direction_masks(sph, smeta, lights, lrec, ds.dmask_n, dmask);
+        }
         ds.off_dmask = off;
         dmask_bytes.resize(dmask.size() * ds.dmask_bytes);
         for (size_t i = 0; i < dmask.size(); ++i)  // little-endian: the low bytes of each mask

@@ -328,7 +328,8 @@ KERNEL_SWITCHES = ["", "-DRT_STATS", "-DRT_CYCLES", "-DRT_PHASE_TRACE", "-DRT_AB
                    "-DRT_ABLATE_TRACE", "-DRT_ABLATE_RAYGEN", "-DRT_ABLATE_FRAMES", "-DRT_WPE0=7",
                    "-DRT_WPE_DEEP=5", "-DRT_WPE2=7", "-DRT_GMASK_TEXELS=32",
                    "-DRT_WPE0_MC=7", "-DRT_FAST_MATH", "-DRT_FAST_DIV", "-DRT_FAST_RSQ",
-                   "-DRT_FAST_SQRT", "-DRT_FAST_POW"]
+                   "-DRT_FAST_SQRT", "-DRT_FAST_POW", "-DRT_UNIFORM_MAT", "-DRT_ABLATE_BOX_PRIMARY",
+                   "-DRT_ABLATE_BOX_SHADOW"]
 
 
 def test_kernel_switch_list_is_complete():
