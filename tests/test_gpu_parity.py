@@ -1462,3 +1462,39 @@ def test_shipped_scene_animated_batch_full_frames(gpu_ctx):
         for r0, r1 in [(0, 4), (300, 308), (716, 720)]:
             o = oracle_render(rt.reference_objects(x), w, h, 0, x, rows=(r0, r1))
             assert np.array_equal(got[k, r0:r1], o), (x, r0, parity_stats(got[k, r0:r1], o))
+
+
+def test_origin_lists_built_on_first_deep_render(gpu_ctx):
+    """The origin-sphere lists are not built by rt_scene_create or
+    rt_scene_update but by the first render that reads them (depth >= 2, a
+    33-256-sphere scene), appended to the device blob (rt_api.cpp
+    ensure_origin_lists): a depth-0 render first, then depth 2, then an
+    update to another scene of the same size and depth 2 again, and a batch
+    of two such scenes; every frame bit-identical to the oracle."""
+    w, h = 192, 108
+    a, b = scenes.bench_objects(100, seed=11), scenes.bench_objects(100, seed=12)
+    sc = rt.Scene(gpu_ctx, a)
+    sb = rt.Scene(gpu_ctx, a)
+    try:
+        f0 = rt.render(gpu_ctx, sc, w, h, 0, time=0.5)
+        assert np.array_equal(f0, oracle_render(a, w, h, 0, 0.5))
+        f2 = rt.render(gpu_ctx, sc, w, h, 2, time=0.5)
+        assert np.array_equal(f2, oracle_render(a, w, h, 2, 0.5)), parity_stats(f2, oracle_render(a, w, h, 2, 0.5))
+        sc.update(b)
+        g2 = rt.render(gpu_ctx, sc, w, h, 2, time=1.5)
+        ob = oracle_render(b, w, h, 2, 1.5)
+        assert np.array_equal(g2, ob), parity_stats(g2, ob)
+        sc.update(a)  # back: the lists of the new contents again
+        # a batch of two scenes of one layout (the same objects), one of them
+        # never rendered: its lists are built by the batch call
+        views = [rt.make_view(None, 0.5), rt.make_view(None, 2.5)]
+        out = dev_zeros((2, h, w, 4), dtype=torch.float32, device="cuda")
+        rt.render_batch_scenes(gpu_ctx, [sc, sb], out.data_ptr(), w, h, 2, views)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert np.array_equal(got[0], f2)
+        oa = oracle_render(a, w, h, 2, 2.5)
+        assert np.array_equal(got[1], oa), parity_stats(got[1], oa)
+    finally:
+        sc.close()
+        sb.close()
