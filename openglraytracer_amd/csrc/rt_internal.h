@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -330,6 +331,20 @@ int check_kernarg_block(hipStream_t stream);
 // rt_api.cpp
 void set_error(const std::string &msg);
 int hip_fail(const char *what, hipError_t e);  // sets the message, returns RT_ERR_HIP
+// The event a render call records after its launch on a caller stream, shared
+// by every scene the call reads (a batch of 256 animated frames with a scene
+// each records one event, not 256: round 6, the shipped workload's host gap
+// of 1.2 ms per launch) and destroyed with its last user (a pending event is
+// released once complete).
+struct UseEvent {
+    hipEvent_t ev = nullptr;
+    UseEvent() = default;
+    UseEvent(const UseEvent &) = delete;
+    UseEvent &operator=(const UseEvent &) = delete;
+    ~UseEvent() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
 int check_render_args(const rt_context *ctx, const rt_scene *scene, int width, int height, int max_depth);
 // launch parameters of n_views views of `scene` on `ctx` (output and rows left to the caller)
 LaunchParams base_params(const rt_context *ctx, const rt_scene *scene, const rt_view *views, int n_views,
@@ -345,7 +360,10 @@ int launch(rt_context *ctx, LaunchParams &p, int max_depth, hipStream_t stream);
 int ensure_origin_lists(rt_context *ctx, const rt_scene *scene, int max_depth);
 // a render on `stream` reads `scene`'s blob: remember it (an event on that
 // stream) so that rt_scene_destroy / rt_scene_update wait for it
-int note_scene_use(const rt_scene *scene, hipStream_t stream);
+// `shared`: the render call's event (created and recorded after its launch
+// by the first scene noted, then reused for the call's other scenes); nullptr:
+// an event of this call alone
+int note_scene_use(const rt_scene *scene, hipStream_t stream, std::shared_ptr<UseEvent> *shared = nullptr);
 // bytes per pixel of a surface format (RT_OUTPUT_*)
 inline size_t surface_bytes(int fmt) { return fmt == RT_OUTPUT_RGBA8 ? 4 : (fmt == RT_OUTPUT_RGB32F ? 12 : 16); }
 
@@ -394,9 +412,10 @@ struct rt_scene {
     // the context's own stream). More than kMaxUseStreams streams: `overflow`,
     // and the release synchronises the device instead.
     static constexpr int kMaxUseStreams = 8;
+    using Event = rtamd::UseEvent;
     struct Use {
         hipStream_t stream;
-        hipEvent_t done;
+        std::shared_ptr<Event> done;
     };
     mutable std::vector<Use> uses;
     mutable bool overflow = false;
