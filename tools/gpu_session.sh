@@ -17,6 +17,7 @@
 #   mix          tools/pmc_mix.sh gpurun_out/TAG/mix $MIX_ARGS (per-wave instruction mix of builds)
 #   shards       tools/shard_timing.py (the N > 1 predictions), to gpurun_out/TAG/shard_timing_latest.json
 #   soak         tools/soak.py $SOAK_SEED $SOAK_N and tools/soak_batch.py $SOAK_SEED2 $SOAK_N2
+#   soakbox      tools/soak.py over many-box scenes (SOAK_KIND=boxes, $SOAK_SEED3 $SOAK_N3)
 #   cycles/stats tools/cycles.py, tools/stats.py (RT_CYCLES / RT_STATS builds)
 #   phase        tools/phase_trace.py (config 2 single-frame phase trace)
 #   acc          tools/ab_accuracy.py $ACC_ARGS
@@ -53,6 +54,7 @@ if want soak; then
   step soak 540 python -u tools/soak.py ${SOAK_SEED:-12000} ${SOAK_N:-400}
   step soak_batch 400 python -u tools/soak_batch.py ${SOAK_SEED2:-12400} ${SOAK_N2:-150}
 fi
+if want soakbox; then step soak_boxes 540 env SOAK_KIND=boxes python -u tools/soak.py ${SOAK_SEED3:-20000} ${SOAK_N3:-300}; fi
 if want cycles; then step cycles 300 python tools/cycles.py cycles ${CYC_ARGS:-config2 config3 config4}; fi
 if want stats; then step stats 300 python tools/stats.py stats ${CYC_ARGS:-config2 config3 config4}; fi
 if want phase; then step phase 300 env PHASE_DUMP=gpurun_out/$tag/phase.npz python tools/phase_trace.py config2 phase; fi

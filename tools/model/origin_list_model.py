@@ -129,6 +129,30 @@ def list_walk(S, per, o, d, t0, slots=None, shell=1):
 
 
 RECORDS = [(15, 4), (15, 1), (27, 4), (27, 9)]
+# (round 6) records as the kernel walks them: (name, slots K, the candidates
+# before which a stored bound is checked, bound quantum): the product's 32-B
+# record (25 slots, uint16 bounds in 1/256 at candidates 8 and 16 and at the
+# end) and a variant of the same 32 B with 24 slots and 8-bit bounds in 1/8
+# units before every 4th candidate (4, 8, ..., 20) and at the end
+KRECORDS = [("product_25_b8_16_q256", 25, (8, 16), 1.0 / 256), ("variant_24_b4_q8", 24, (4, 8, 12, 16, 20), 1.0 / 8)]
+
+
+def list_walk_k(S, per, o, d, t0, slots, checks, q):
+    """The kernel's record walk: the lane tests candidates 0..K-1, stopping
+    before candidate i in `checks` (and at the end) when its closest hit is
+    below the stored bound floor(b / q) q; past the record with candidates
+    left and the end bound not reached: the BVH. Returns (tests, fallback)."""
+    js, b = per
+    best, tests = t0, 0
+    n = min(len(js), slots)
+    for i in range(n):
+        if i in checks and np.floor(b[i] / q) * q > best:
+            return tests, False
+        tests += 1
+        best = min(best, sphere_hit(S, js[i], o, d))
+    if len(js) > slots and not (best < np.floor(b[slots] / q) * q):
+        return tests, True
+    return tests, False
 
 
 def main():
@@ -184,6 +208,22 @@ def main():
                 tot["list_tests"] += n_t
                 longest = max(longest, n_t)
             tot["list_passes"] += longest
+            for name, K, checks, q in KRECORDS:
+                r = tot.setdefault(name, dict(passes=0, iters=0, sp=0, fallback=0))
+                longest, fb = 0, []
+                for i in sph_lanes:
+                    nd = lanes[i]
+                    n_t, f = list_walk_k(S, lists[int(src[nd])][tex[i]], ro[nd], rd[nd], tb[i], K, checks, q)
+                    longest = max(longest, n_t)
+                    if f:
+                        fb.append(i)
+                r["passes"] += longest
+                r["fallback"] += len(fb)
+                bl = box_lanes + fb
+                if bl:
+                    it3, ps3, _, _ = bm.lane_walk(B, [rays[i] for i in bl], [tb[i] for i in bl])
+                    r["iters"] += it3
+                    r["sp"] += ps3
             # fixed records: K slots, a stored bound every `shell` candidates
             for K, sh in RECORDS:
                 key = "rec%d_s%d" % (K, sh)
@@ -222,10 +262,16 @@ def main():
             "list_passes": round(r["passes"] / c, 2), "bvh_node_iters": round(r["iters"] / c, 2),
             "bvh_sphere_passes": round(r["sp"] / c, 2),
             "fallback_share_of_sphere_rays": round(r["fallback"] / max(1, tot["sphere_rays"]), 4)}
+    for name, K, checks, q in KRECORDS:
+        r = tot[name]
+        out["per_wave_call"][name] = {
+            "list_passes": round(r["passes"] / c, 2), "bvh_node_iters": round(r["iters"] / c, 2),
+            "bvh_sphere_passes": round(r["sp"] / c, 2),
+            "fallback_share_of_sphere_rays": round(r["fallback"] / max(1, tot["sphere_rays"]), 4)}
     bt = out["per_wave_call"]["bvh_today"]
     out["units_per_wave_call"] = {"bvh_today": round(bt["node_iters"] + bt["sphere_passes"], 2)}
     for k, v in out["per_wave_call"].items():
-        if k.startswith("record"):
+        if k.startswith(("record", "product", "variant")):
             out["units_per_wave_call"][k] = round(v["list_passes"] + v["bvh_node_iters"] + v["bvh_sphere_passes"], 2)
     print(json.dumps(out))
 

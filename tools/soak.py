@@ -3,6 +3,8 @@ scenes (tests/test_gpu_parity.py random_scene, larger frames) through the HIP
 kernel against the oracle, bit for bit, culling on and off.
 
     python tools/soak.py FIRST_SEED N [MAX_W MAX_H]
+    SOAK_KIND=boxes python tools/soak.py ...   (tests/test_gpu_parity.py box_scene:
+                                               4-12 rotated boxes, round 6's box culling)
 """
 import os
 import sys
@@ -15,14 +17,16 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: F401,E402  (HIP runtime first)
 import openglraytracer_amd as rt  # noqa: E402
 from oracle import port  # noqa: E402
-from test_gpu_parity import random_scene  # noqa: E402
+from test_gpu_parity import box_scene, random_scene  # noqa: E402
+
+make_scene = box_scene if os.environ.get("SOAK_KIND") == "boxes" else random_scene
 
 first, n = int(sys.argv[1]), int(sys.argv[2])
 max_w, max_h = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (200, 150)
 ctx = rt.Context(0)
 bad, pixels, rays_depth, olist = [], 0, {}, 0
 for seed in range(first, first + n):
-    objs, mats, lights, t, depth, w, h = random_scene(seed)
+    objs, mats, lights, t, depth, w, h = make_scene(seed)
     rng = np.random.default_rng(seed)
     w, h = int(rng.integers(w, max_w + 1)), int(rng.integers(h, max_h + 1))
     view = rt.make_view(None, t)
