@@ -249,6 +249,9 @@ struct LaunchParams {
     int32_t off_olist;
     // 1: the LDS direction masks carry a bit per box (bit n_spheres + b)
     int32_t dmask_box;
+    // per (box, light) a plane that separates the box from the light's end
+    // of every shadow segment (rt_scene.cpp), 16-B units; -1: none
+    int32_t off_bplane;
     // host only (the kernels never read it): 1 when every view of the launch
     // culls, so the depth-0 kernels may take the scene's shape (scene_shape)
     int32_t shape_cull;
@@ -283,6 +286,7 @@ struct DeviceScene {
     int32_t off_bvh = 0, n_bvh = 0, off_blink = 0, off_cone = 0;
     int32_t off_dmask = -1, dmask_n = 0, dmask_bytes = 4;
     int32_t dmask_box = 0;  // the LDS masks carry a bit per box, bit n_spheres + b (round 6)
+    int32_t off_bplane = -1;  // n_boxes x n_lights separating planes (float4), 16-B units; -1: none (round 6)
     int32_t off_gmask = -1, gmask_words = 0, off_glist = -1;
     int32_t off_olist = -1;   // -1 until the lists are built (ensure_origin_lists)
     int32_t olist_eligible = 0;  // kOListMinSpheres..256 spheres: depth >= 2 renders get the lists

@@ -369,6 +369,9 @@ struct Scene {
     const char *dmask;  // [live light][face][row][col] shadow direction masks (nullptr: none)
     int dmask_n, dmask_bytes;
     int dmask_box;  // the masks carry a bit per box (bit ns + b)
+    // per (box, light) the plane separating the box from the light's end of
+    // every shadow segment (rt_scene.cpp; nullptr: none, or culling off)
+    const __attribute__((address_space(4))) float4 *cbplane;
     const uint64_t *gmask;  // wide masks in global memory: [live light][texel][word] (nullptr: none)
     const uint4 *glist;     // their candidate lists: [live light][texel] (nullptr: none)
     int gwords;
@@ -897,8 +900,16 @@ __device__ __forceinline__ bool occluded_impl(const Scene &S, v3 start, v3 dir, 
 #ifdef RT_ABLATE_BOX_SHADOW
         if (!S.room && b > 0) continue;  // (timing probe: wrong images by design)
 #endif
-        if (box_bits) {
-            const bool cand = need && !hit && ((mask >> (S.ns + b)) & 1u) != 0u;
+        if (box_bits || S.cbplane) {
+            bool cand = need && !hit;
+            if (box_bits) cand = cand && ((mask >> (S.ns + b)) & 1u) != 0u;
+            if (S.cbplane) {
+                // the segment's start beyond the plane of the box's face that
+                // the light lies beyond: both ends beyond, no occluder (the
+                // host's margins cover this float evaluation, rt_scene.cpp)
+                const float4 pl = cload(S.cbplane + (b * S.nl + light));
+                cand = cand && !(start.x * pl.x + start.y * pl.y + start.z * pl.z + pl.w > 0.0f);
+            }
             if (!wave_any(cand)) continue;
             const bool occ = box_occludes(cload(S.cbox + b), start, dir, light_bit, S.room != 0, S.cull != 0);
             hit = hit | (cand & occ);
@@ -1770,6 +1781,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
     S.room = 0;
+    if (!S.cull) S.cbplane = nullptr;  // (culling off: every box tested)
     // the scene's shape as constants (scene_shape checked it on the host):
     // every feature test on the path folds, and with a room (one box) every
     // loop over the boxes and the shadow queries' box shortcut test
@@ -1799,6 +1811,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
         S.nb = 1;
         S.room = 1;
         S.dmask_box = 0;  // (a room scene's masks carry no box bits: rt_scene.cpp)
+        S.cbplane = nullptr;  // (nor separating planes: one box)
     }
     RT_CYC(kCycRaygen);
     if (!wave_any(px.active)) return;
@@ -1980,6 +1993,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     S.dmask_n = p.dmask_n;
     S.dmask_bytes = p.dmask_bytes;
     S.dmask_box = p.dmask_box;
+    S.cbplane = p.off_bplane >= 0 ? (const __attribute__((address_space(4))) float4 *)(blob + p.off_bplane) : nullptr;
     // (recursive depths only: the depth-0/1 kernels keep their register
     // budget and use the per-wave cone for such scenes)
     S.gmask = kDepth >= 2 && p.off_gmask >= 0 ? reinterpret_cast<const uint64_t *>(blob + p.off_gmask) : nullptr;

@@ -1178,6 +1178,51 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     ds.off_mats = off;    off += units(mrec.size() * sizeof(MatRec));
     ds.off_lights = off;  off += units(lrec.size() * sizeof(LightRec));
     ds.off_lightmat = off; off += units(lm.size() * sizeof(LightMatRec));
+    // Round 6: in a scene of several boxes (chosen by the object kinds alone,
+    // as the mask bits), per (box, light) the face plane of the box (in the
+    // float32 transform the kernel uses) with the light farthest beyond it:
+    // a shadow segment whose start lies beyond that plane too cannot be
+    // occluded by the box (both of its ends beyond the plane of a face; the
+    // exact slab test then sees that axis' entry at t > 1 or a miss). Stored
+    // as (n, w) with the margin m folded into w (a start counts as beyond
+    // when n . start + w > 0), m = 1e-3 + 1e-5 (scene extent + |w|), far
+    // above the float32 rounding of n . start and of the kernel's transform;
+    // kept only if the light lies beyond by more than 0.01 (the segment ends
+    // at L + 0.01 n, :808-809) + 2 m; else w = -inf (never beyond).
+    std::vector<float4> bplane;
+    ds.off_bplane = -1;
+    if (boxes.size() >= 2) {
+        bool finite = true;  // (a non-finite object: no planes; shaded points are bounded by `extent` otherwise)
+        for (int i = 0; i < n_objs; ++i)
+            for (int k = 0; k < 3; ++k)
+                finite = finite && std::isfinite(objs[i].position[k]) && std::isfinite(objs[i].box_mins[k]) &&
+                         std::isfinite(objs[i].box_maxs[k]) && std::isfinite(objs[i].radius);
+        bplane.assign(boxes.size() * static_cast<size_t>(n_lights), float4{0.0f, 0.0f, 0.0f, -HUGE_VALF});
+        for (size_t b = 0; b < boxes.size() && finite; ++b) {
+            const BoxRec &B = boxes[b];
+            for (int j = 0; j < n_lights; ++j) {
+                const double L[3] = {lights[j].position[0], lights[j].position[1], lights[j].position[2]};
+                double best = -HUGE_VAL, bn[3] = {0, 0, 0}, bw = 0, bm = 0;
+                for (int a = 0; a < 3; ++a)
+                    for (int sgn = -1; sgn <= 1; sgn += 2) {
+                        const double face = sgn > 0 ? B.maxs[a] : B.mins[a];
+                        const double r[4] = {B.w2l[4 * a], B.w2l[4 * a + 1], B.w2l[4 * a + 2], B.w2l[4 * a + 3]};
+                        const double sl = sgn * (r[0] * L[0] + r[1] * L[1] + r[2] * L[2] + r[3] - face);
+                        if (sl > best) {
+                            best = sl;
+                            for (int k = 0; k < 3; ++k) bn[k] = sgn * r[k];
+                            bw = sgn * (r[3] - face);
+                            bm = 1e-3 + 1e-5 * (extent + std::fabs(r[3]) + std::fabs(face));
+                        }
+                    }
+                if (std::isfinite(best) && std::isfinite(bw) && best > 0.01 + 2.0 * bm)
+                    bplane[b * n_lights + j] = float4{static_cast<float>(bn[0]), static_cast<float>(bn[1]),
+                                                      static_cast<float>(bn[2]), static_cast<float>(bw - bm)};
+            }
+        }
+        ds.off_bplane = off;
+        off += units(bplane.size() * sizeof(float4));
+    }
     ds.off_bvh = off;     off += units(bvh.size() * sizeof(BvhNode));
     ds.off_blink = off;   off += units(blink.size() * sizeof(uint32_t));
     // The cone table rides in LDS only while the work-group's LDS stays small
@@ -1367,6 +1412,7 @@ int build_scene(const rt_object *objs, int n_objs, const rt_material *mats, int 
     put(ds.off_mats, mrec.data(), mrec.size() * sizeof(MatRec));
     put(ds.off_lights, lrec.data(), lrec.size() * sizeof(LightRec));
     put(ds.off_lightmat, lm.data(), lm.size() * sizeof(LightMatRec));
+    if (ds.off_bplane >= 0) put(ds.off_bplane, bplane.data(), bplane.size() * sizeof(float4));
     put(ds.off_bvh, bvh.data(), bvh.size() * sizeof(BvhNode));
     put(ds.off_blink, blink.data(), blink.size() * sizeof(uint32_t));
     if (ds.off_cone >= 0) put(ds.off_cone, cones.data(), cones.size() * sizeof(ShadowCone));
