@@ -241,6 +241,17 @@ def valu_bound(pmc, kernel_ms):
     return out
 
 
+def check_traffic(pmc, stored):
+    """A launch stores every pixel once, so a PMC summary whose WRITE_SIZE is
+    below the launch's stored bytes belongs to another launch shape (round
+    5's mixed-shape averages): returns (pmc or {}, the check record or None)."""
+    if pmc.get("write_bytes_per_launch") is None:
+        return pmc, None
+    rec = {"write_bytes_per_launch": pmc["write_bytes_per_launch"], "stored_bytes_per_launch": stored,
+           "ok": pmc["write_bytes_per_launch"] >= 0.99 * stored}
+    return (pmc if rec["ok"] else {}), rec
+
+
 LINK_GBPS = (50.0, 100.0)  # per-direction rate RCCL may reach on one xGMI link (nominal ≈150 GB/s)
 
 
@@ -1040,15 +1051,11 @@ def main():
     # bytes than the launch stores belongs to another launch shape (round 5's
     # mixed-shape average), so none of its figures is this launch's
     stored = plan.px_per_launch * plan.bytes_per_pixel
-    traffic_check = None
-    if pmc.get("write_bytes_per_launch") is not None:
-        traffic_check = {"write_bytes_per_launch": pmc["write_bytes_per_launch"], "stored_bytes_per_launch": stored,
-                         "ok": pmc["write_bytes_per_launch"] >= 0.99 * stored}
-        if not traffic_check["ok"]:
-            sys.stderr.write("bench.py: profiles/pmc_%s_latest.json writes %.4g B per launch, below the %.4g B the "
-                             "launch stores: not this launch shape's counters; traffic and valu left out\n"
-                             % (wl, pmc["write_bytes_per_launch"], stored))
-            pmc = {}
+    pmc, traffic_check = check_traffic(pmc, stored)
+    if traffic_check is not None and not traffic_check["ok"]:
+        sys.stderr.write("bench.py: profiles/pmc_%s_latest.json writes %.4g B per launch, below the %.4g B the "
+                         "launch stores: not this launch shape's counters; traffic and valu left out\n"
+                         % (wl, traffic_check["write_bytes_per_launch"], stored))
     traffic = pmc.get("hbm_bytes_per_launch")
     if rank == 0:
         cpu = None

@@ -94,3 +94,18 @@ def test_committed_summaries_write_what_they_store(workload):
     stored = cfg["width"] * cfg["height"] * 16 * d.get("frames_per_launch", 1)
     assert d["write_bytes_per_launch"] >= 0.99 * stored, (d["write_bytes_per_launch"], stored)
     assert "dispatch_selection" in d
+
+
+def test_bench_refuses_a_summary_that_writes_less_than_it_stores():
+    """bench.py's traffic check: round 5's config-2 summary (8.056 GB written
+    for a 256-frame launch that stores 8.493 GB) is left out of the line;
+    the round-6 one (8.493 GB) is kept."""
+    sys.path.insert(0, ROOT)
+    import bench
+    stored = 256 * 1920 * 1080 * 16
+    pmc, rec = bench.check_traffic({"write_bytes_per_launch": 8.056e9, "hbm_bytes_per_launch": 8.058e9}, stored)
+    assert pmc == {} and rec["ok"] is False
+    good = {"write_bytes_per_launch": 8493465600.0, "hbm_bytes_per_launch": 8.4955e9}
+    pmc, rec = bench.check_traffic(good, stored)
+    assert pmc is good and rec["ok"] is True
+    assert bench.check_traffic({}, stored) == ({}, None)
