@@ -40,9 +40,10 @@ launch). The total work of a step is fixed: strong scaling.
     the assembling rank's own whole-frame render byte for byte.
 
 config3 at N=1 (3840x2160 / 64 spheres / depth 2): a step is
-F frames of the animated loop (--frames, default 7: the views one queued
+F frames of the animated loop (--frames, default: the views one queued
 launch holds for this scene, every view's frame constants beside the scene
-in LDS), rendered in one rt_render_batch launch whose wave tiles are taken
+in LDS — 5 at the depth-2 kernel's 7 waves per SIMD, 7 at round 5's 6),
+rendered in one rt_render_batch launch whose wave tiles are taken
 view after view from the queues, so the launch's tail is paid once per F
 frames; `single_frame` is the same frames one per launch.
 
@@ -135,7 +136,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
     ap.add_argument("--frames", type=int, default=None,
-                    help="config2 (default 256) and config3 at N=1 (default 7): animated frames per step, up to "
+                    help="config2 (default 256) and config3 at N=1 (default: the views one queued launch holds, 5 at "
+                         "7 waves per SIMD): animated frames per step, up to "
                          "256 per rt_render_batch call (SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
     ap.add_argument("--frame-exchange", choices=["spread", "gather", "all_to_all", "none"], default="spread",
                     help="config2 at N>1: spread (default) = every frame of the step row-tiled over the ranks, "
@@ -405,13 +407,17 @@ def main():
 
     ctx = rt.Context(device)
     wl = args.workload
-    F = args.frames or (7 if wl == "config3" else 256)
+    # (config3 at N = 1: F = the views one queued launch holds beside the
+    # scene in LDS, found below once the scene exists)
+    F = args.frames or (0 if wl == "config3" and world == 1 else 7 if wl == "config3" else 256)
     scenes = None  # shipped: frame k's own scene (the reference's objects at t = k/60 s)
     if wl == "shipped":
         scenes = [rt.Scene(ctx, rt.reference_objects(frame_time(k))) for k in range(F)]
         scene = scenes[0]
     else:
         scene = rt.Scene(ctx, rt.bench_objects(cfg["spheres"], 0))
+    if F == 0:  # config3 at N = 1: one queued launch per step
+        F = max(k for k in range(1, 65) if rt.batch_launches(ctx, scene, k, DEPTH) == 1)
     ctx.set_timing(False)  # no per-launch markers of the library's own
     # Streams of our own: renders are launched asynchronously on `render_s`
     # (the C-ABI treats a NULL stream — torch's default stream handle is 0 —

@@ -1634,10 +1634,15 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #define RT_WPE_DEEP 6
 #endif
 #ifndef RT_WPE2
-// depth 2 (config 3): 7 waves timed 0.878 vs 0.893 ms in short bursts (r03b),
-// but raised the HBM traffic 2.4 -> 4.1 GB per frame (216 B of scratch per
-// lane) and the sustained bench kernel to 1.03 ms at a 1.99 GHz clock (r03c)
-#define RT_WPE2 6
+// depth 2 (config 3) at 7 waves (72 VGPRs): on round 3's walk it raised the
+// HBM traffic 2.4 -> 4.1 GB per frame and the sustained bench kernel to
+// 1.03 ms against 0.98 (r03c); on round 6's (split frames, origin lists,
+// scene shapes: 176 B of scratch per lane against 152 at 6 waves) the
+// interleaved bench lines take 4.538 -> 4.418-4.428 ms per 7-frame step
+// (-2.6 %; the launch then holds 5 views beside the scene in LDS, so the
+// step is two launches, 4 + 3), frames verified (profiles/r06v/); depth 4
+// at 7 waves stays +0.8 %, at 5 +9 % (profiles/r06u_ab_deep_occupancy.log)
+#define RT_WPE2 7
 #endif
 #define RT_WAVES_PER_EU(d) ((d) == 2 ? RT_WPE2 : ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1)))
 #endif

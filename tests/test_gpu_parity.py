@@ -931,15 +931,17 @@ def test_config5_monte_carlo_kernel_full_frame(gpu_ctx):
 
 
 def test_split_deep_batch_is_counted_and_timed_whole(gpu_ctx):
-    """A deep batch larger than one queued launch holds (7 views of the
-    64-sphere scene) runs as several launches: rt_batch_launches says how
-    many, and rt_last_kernel_ms covers all of them, not the last one only."""
+    """A deep batch larger than one queued launch holds (5 views of the
+    64-sphere scene at the depth-2 kernel's 7 waves per SIMD) runs as several
+    launches: rt_batch_launches says how many, and rt_last_kernel_ms covers
+    all of them, not the last one only."""
     objs = scenes.bench_objects(64)
     w, h, depth = 1280, 720, 2
     sc = rt.Scene(gpu_ctx, objs)
     try:
-        cap = 7
-        assert rt.batch_launches(gpu_ctx, sc, cap, depth) == 1
+        cap = max(k for k in range(1, 65) if rt.batch_launches(gpu_ctx, sc, k, depth) == 1)
+        assert 2 <= cap < 64
+        assert rt.batch_launches(gpu_ctx, sc, cap + 1, depth) == 2
         assert rt.batch_launches(gpu_ctx, sc, 3 * cap, depth) == 3
         assert rt.batch_launches(gpu_ctx, sc, 3 * cap, 0) == 1
         views = [rt.make_view(None, k / 60.0) for k in range(3 * cap)]

@@ -27,7 +27,9 @@ if [ "$what" = prof ] || [ "$what" = all ]; then
   run prof_config5 900 tools/profile.sh $tag/c5 --workload config5 --steps 2 --warmup 1
   run prof_shipped 900 tools/profile.sh $tag/cs --workload shipped --steps 50 --warmup 5
   run sum2 60 python tools/pmc_summary.py $out/c2 profiles/${tag}_config2 256 config2 --skip 5
-  run sum3 60 python tools/pmc_summary.py $out/c3 profiles/${tag}_config3 7 config3 --skip 2
+  # config 3's step is one queued launch of the views it holds (bench.py): its frame count
+  f3=$(timeout -k 10 120 python -c "import openglraytracer_amd as rt; c = rt.Context(0); s = rt.Scene(c, rt.bench_objects(64, 0)); print(max(k for k in range(1, 65) if rt.batch_launches(c, s, k, 2) == 1))") || exit 1
+  run sum3 60 python tools/pmc_summary.py $out/c3 profiles/${tag}_config3 $f3 config3 --skip 2
   run sum4 60 python tools/pmc_summary.py $out/c4 profiles/${tag}_config4 1 config4 --skip 1
   run sum5 60 python tools/pmc_summary.py $out/c5 profiles/${tag}_config5 1 config5 --skip 1
   run sums 60 python tools/pmc_summary.py $out/cs profiles/${tag}_shipped 256 shipped --skip 5
