@@ -256,6 +256,11 @@ struct LaunchParams {
     // culls, so the depth-0 kernels may take the scene's shape (scene_shape)
     int32_t shape_cull;
     int32_t scene_room;  // host only: every scene of the launch is a room (DeviceScene::room)
+    // 1 (set by launch_kernel for the wide-shape recursive kernels): a view's
+    // records in LDS are its footprints and box terms only, not the spheres'
+    // camera terms (the primary rays compute them as secondary rays do: the
+    // same arithmetic, so the same values) — 16 B less per sphere per view
+    int32_t lean_views;
 };
 // ROCm passes kernel arguments above 4 KiB (an 8 KB argument block checked on
 // MI355X); this block stays under 6 KiB.
@@ -274,6 +279,11 @@ constexpr int kShapeMaskTexels = 12;  // the LDS masks' texels per face edge in 
 constexpr int kShapeRoom = 16;
 constexpr int kShapeWide = 32;
 int scene_shape(const LaunchParams &p, int max_depth);
+// Lean views (LaunchParams::lean_views): the wide-shape kernels.
+constexpr bool kLeanViews(int shape) { return (shape & kShapeWide) != 0; }
+// 16-B records of one view's per-frame constants in LDS: the spheres' camera
+// terms (not with lean views) and footprints, the boxes' camera terms.
+inline int view_units(const LaunchParams &p) { return (p.lean_views ? 1 : 2) * p.n_spheres + p.n_boxes; }
 constexpr int kQueues = 32;                            // wave-tile queues of a queued launch
 constexpr int kQueueStride = 64;                       // ints: each counter on a 256-B line of its own
 constexpr int kSchedInts = 2 * kQueues * kQueueStride; // heads + done counters of one launch

@@ -357,6 +357,7 @@ struct Scene {
     const float4 *sph;      // cx, cy, cz, r*r
     const int4 *smeta;      // obj_index, material, radius bits, 0
     const float4 *sph_cam;  // camera-origin terms: oc = origin - centre, qc (:587-588)
+    int cam_terms;          // sph_cam present (a constant per kernel: not with lean views)
     const int4 *sph_px;     // conservative pixel footprint x0, x1, y0, y1 (culling)
     const BoxRec *box;
     const float4 *box_cam;  // box-local camera origin (:655), w = origin strictly inside
@@ -742,7 +743,8 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
                 const int s = base + __builtin_ctzll(mask);
                 mask &= mask - 1;
                 RT_STAT(6, true);
-                test_sphere(S, s, r.start, d2, qa2, qa4, floor, true, h);
+                // (lean views: the camera terms computed here, as for secondary rays)
+                test_sphere(S, s, r.start, d2, qa2, qa4, floor, S.cam_terms != 0, h);
             }
         }
     } else if (!kPrimary && S.cull && S.nbvh > 0) {
@@ -833,7 +835,7 @@ __device__ __forceinline__ Hit closest_impl(const Scene &S, const Ray &r, bool v
             }
         }
     } else {
-        for (int s = 0; s < S.ns; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, floor, kPrimary, h);
+        for (int s = 0; s < S.ns; ++s) test_sphere(S, s, r.start, d2, qa2, qa4, floor, kPrimary && S.cam_terms != 0, h);
     }
     if (!valid) h.obj = -1;
     return h;
@@ -1624,8 +1626,9 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 
 // Occupancy target per depth: the recursive kernels (depth >= 2) keep the
 // tree walk's frames in scratch either way and hide its latency best at 6
-// waves per SIMD (config 4: 58 -> 37 ms; config 3: 1.52 -> 1.37 ms); depth 0/1
-// need fewer registers than that anyway.
+// (the general kernels) or 7 (the wide shapes, round 6) waves per SIMD
+// (config 4: 58 -> 37 ms from the uncapped build to 6; config 3: 1.52 ->
+// 1.37 ms); depth 0/1 need fewer registers than that anyway.
 #ifndef RT_WAVES_PER_EU
 #ifndef RT_WPE0
 #define RT_WPE0 8  // depth 0 at 64 VGPRs (measured equal to the unconstrained 70: 42.9 us per 1080p frame either way)
@@ -1634,17 +1637,25 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #define RT_WPE_DEEP 6
 #endif
 #ifndef RT_WPE2
-// depth 2 (config 3) at 7 waves (72 VGPRs): on round 3's walk it raised the
-// HBM traffic 2.4 -> 4.1 GB per frame and the sustained bench kernel to
-// 1.03 ms against 0.98 (r03c); on round 6's (split frames, origin lists,
-// scene shapes: 176 B of scratch per lane against 152 at 6 waves) the
-// interleaved bench lines take 4.538 -> 4.418-4.428 ms per 7-frame step
-// (-2.6 %; the launch then holds 5 views beside the scene in LDS, so the
-// step is two launches, 4 + 3), frames verified (profiles/r06v/); depth 4
-// at 7 waves stays +0.8 %, at 5 +9 % (profiles/r06u_ab_deep_occupancy.log)
-#define RT_WPE2 7
+// depth 2, general kernel: 7 waves had raised round 3's HBM traffic 2.4 ->
+// 4.1 GB per frame and its sustained bench kernel to 1.03 ms against 0.98 (r03c)
+#define RT_WPE2 6
 #endif
-#define RT_WAVES_PER_EU(d) ((d) == 2 ? RT_WPE2 : ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1)))
+#ifndef RT_WPE_WIDE
+// the wide-shape recursive kernels (configs 3-4) at 7 waves (72 VGPRs),
+// re-measured on round 6's walk (split frames, origin lists, lean views):
+// config 3 (depth 2; 176 B of scratch per lane against 152) 4.538 ->
+// 4.418-4.428 ms per 7-frame step in interleaved bench lines (-2.6 %,
+// profiles/r06v/), its queued launch then holding 5 views beside the scene;
+// config 4 (depth 4; 252 B against 232) +0.8 % while its 24.5 KB of LDS per
+// work-group held it at 6 work-groups per CU (profiles/r06u_*), 10.28 ->
+// 9.81 ms (-4.6 %) once lean views (20.5 KB) let the seventh in
+// (profiles/r06y_ab_lean_views.log); 5 waves +9 %
+#define RT_WPE_WIDE 7
+#endif
+#define RT_WAVES_PER_EU(d, shape) \
+    (((d) >= 2 && ((shape) & kShapeWide) != 0) ? RT_WPE_WIDE \
+     : (d) == 2 ? RT_WPE2 : ((d) >= 2 ? RT_WPE_DEEP : ((d) == 0 ? RT_WPE0 : 1)))
 #endif
 #ifndef RT_WPE0_MC
 // depth-0 Monte-Carlo kernel (config 5): 6 waves, 80 VGPRs + 16 B scratch:
@@ -1653,7 +1664,7 @@ __device__ __forceinline__ float jitter_u(uint32_t seed, uint32_t sample, uint32
 #define RT_WPE0_MC 6
 #endif
 #define RT_OCCUPANCY \
-    __attribute__((amdgpu_waves_per_eu((kAccum && kDepth == 0) ? RT_WPE0_MC : RT_WAVES_PER_EU(kDepth))))
+    __attribute__((amdgpu_waves_per_eu((kAccum && kDepth == 0) ? RT_WPE0_MC : RT_WAVES_PER_EU(kDepth, kShape))))
 // Reductions over aligned groups of 8 lanes (DPP: quad butterflies, then the
 // half-row mirror); every lane of the group ends with the result.
 __device__ __forceinline__ float group8_min(float v) {
@@ -1697,7 +1708,7 @@ __device__ __forceinline__ void frame_setup(const LaunchParams &p, const FrameVi
         const bool ok = group8_min(ok_i ? 1.0f : 0.0f) == 1.0f;  // every corner in front of the camera
         if (i == 0) {
             const v3 oc = sub(origin, mk(c.x, c.y, c.z));
-            sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);
+            if (sph_cam) sph_cam[s] = make_float4(oc.x, oc.y, oc.z, dot(oc, oc) - c.w);  // (lean views: none)
             // pixel x <-> NDC (x - hw) / hw (:377); two pixels of margin
             const float fx0 = floorf(x0 * hw + hw) - 2.0f, fx1 = ceilf(x1 * hw + hw) + 2.0f;
             const float fy0 = floorf(y0 * hh + hh) - 2.0f, fy1 = ceilf(y1 * hh + hh) + 2.0f;
@@ -1786,6 +1797,7 @@ __device__ __forceinline__ void render_wave_tile(const LaunchParams &p, Scene S,
                                                  int z, const Pixel &px, const Ray &pre, bool have_pre) {
     S.cull = V.cull;
     S.room = 0;
+    S.cam_terms = kLeanViews(kShape) ? 0 : 1;
     if (!S.cull) S.cbplane = nullptr;  // (culling off: every box tested)
     // the scene's shape as constants (scene_shape checked it on the host):
     // every feature test on the path folds, and with a room (one box) every
@@ -1942,9 +1954,14 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     // view's fit in the kernel arguments: host_frame_setup) — else derived
     // below by every work-group
     static_assert(kMaxViewConsts <= kThreads, "one record per thread");
-    if (tid < p.n_frame_consts) fc = (kDev ? p.consts_dev : p.frame_consts)[z * p.n_frame_consts + tid];
-    float4 *sph_cam = lds + p.blob_units;
-    int4 *sph_px = reinterpret_cast<int4 *>(sph_cam + p.n_spheres);
+    // lean views (the wide shapes, kLeanViews): the host's records of a view
+    // minus their first n_spheres (the camera terms) go to LDS
+    constexpr bool kLean = kLeanViews(kShape);
+    const int skip = kLean ? p.n_spheres : 0, keep = p.n_frame_consts - skip;
+    if (tid < keep) fc = (kDev ? p.consts_dev : p.frame_consts)[z * p.n_frame_consts + skip + tid];
+    float4 *const views = lds + p.blob_units;  // view k's records at views + k * view_units
+    float4 *sph_cam = kLean ? nullptr : views;
+    int4 *sph_px = reinterpret_cast<int4 *>(views + (kLean ? 0 : p.n_spheres));
     float4 *box_cam = reinterpret_cast<float4 *>(sph_px + p.n_spheres);
     const int own_wx = static_cast<int>(blockIdx.x) * kWavesX + wave % kWavesX;
     const int own_wy = static_cast<int>(blockIdx.y) * kWavesY + wave / kWavesX;
@@ -1957,18 +1974,24 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     if (tid < p.blob_units) lds[tid] = first;
     RT_PHASE(11);
     for (int i = tid + kThreads; i < p.blob_units; i += kThreads) lds[i] = blob[i];
-    // (queued: view k's records at sph_cam + k * view_units)
-    const int view_units = 2 * p.n_spheres + p.n_boxes;
+    const int view_units = (kLean ? 1 : 2) * p.n_spheres + p.n_boxes;
     if (p.n_frame_consts > 0) {
-        if (tid < p.n_frame_consts) sph_cam[tid] = fc;
-        for (int i = tid + p.n_frame_consts; i < n_staged * p.n_frame_consts; i += kThreads)
-            sph_cam[i] = p.frame_consts[i];
+        if (tid < keep) views[tid] = fc;
+        if (kLean) {
+            for (int i = tid + keep; i < n_staged * keep; i += kThreads) {
+                const int k = i / keep;
+                views[i] = p.frame_consts[k * p.n_frame_consts + skip + (i - k * keep)];
+            }
+        } else {
+            for (int i = tid + p.n_frame_consts; i < n_staged * p.n_frame_consts; i += kThreads)
+                views[i] = p.frame_consts[i];
+        }
     } else {
         frame_setup(p, V, sph_cam, sph_px, box_cam);
         for (int k = 1; k < n_staged; ++k) {
-            float4 *c = sph_cam + k * view_units;
-            int4 *px = reinterpret_cast<int4 *>(c + p.n_spheres);
-            frame_setup(p, p.view[k], c, px, reinterpret_cast<float4 *>(px + p.n_spheres));
+            float4 *c = views + k * view_units;
+            int4 *px = reinterpret_cast<int4 *>(c + (kLean ? 0 : p.n_spheres));
+            frame_setup(p, p.view[k], kLean ? nullptr : c, px, reinterpret_cast<float4 *>(px + p.n_spheres));
         }
     }
     RT_PHASE(12);
@@ -2038,8 +2061,9 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
         const int wx = queued ? r % wtx : own_wx, wy = queued ? r / wtx : own_wy;
         Scene St = S;
         if (queued && zt != 0) {
-            St.sph_cam = sph_cam + zt * view_units;
-            St.sph_px = reinterpret_cast<const int4 *>(St.sph_cam + p.n_spheres);
+            const float4 *c = views + zt * view_units;
+            St.sph_cam = kLean ? nullptr : c;
+            St.sph_px = reinterpret_cast<const int4 *>(c + (kLean ? 0 : p.n_spheres));
             St.box_cam = reinterpret_cast<const float4 *>(St.sph_px + p.n_spheres);
         }
         render_wave_tile<kDepth, kAccum, kShape>(p, St, queued ? p.view[zt] : V, wx, wy, zt,
@@ -2086,7 +2110,7 @@ int groups_per_cu(const void *fn, size_t lds) {
 // LDS of a queued launch of n views: the scene and every view's per-frame
 // constants.
 size_t queued_lds_bytes(const LaunchParams &p, int n) {
-    return lds_bytes(p) + static_cast<size_t>(n - 1) * (2 * p.n_spheres + p.n_boxes) * sizeof(float4);
+    return lds_bytes(p) + static_cast<size_t>(n - 1) * view_units(p) * sizeof(float4);
 }
 
 // Views of one scene a queued launch holds at the one-view launch's resident
@@ -2102,7 +2126,7 @@ int queued_views_for(const void *fn, const LaunchParams &p) {
     thread_local Entry cache[8] = {};
     thread_local int next = 0;
     const size_t lds = lds_bytes(p);
-    const int units = 2 * p.n_spheres + p.n_boxes;
+    const int units = view_units(p);
     for (const Entry &e : cache)
         if (e.fn == fn && e.lds == lds && e.units == units && e.n > 0) return e.n;
     const int g1 = groups_per_cu(fn, lds);
@@ -2117,6 +2141,7 @@ int queued_views_for(const void *fn, const LaunchParams &p) {
 
 template <int kDepth, bool kAccum, bool kDev = false, int kShape = 0>
 hipError_t launch_kernel(LaunchParams &p, hipStream_t stream) {
+    p.lean_views = kLeanViews(kShape) ? 1 : 0;
     size_t lds = lds_bytes(p);
     const void *fn = reinterpret_cast<const void *>(&render_kernel<kDepth, kAccum, kDev, kShape>);
     dim3 grid((p.width + kTileX - 1) / kTileX, (p.slice_rows + kTileY - 1) / kTileY, p.n_views);
@@ -2201,8 +2226,9 @@ int scene_shape(const LaunchParams &p, int max_depth) {
 }
 
 size_t lds_bytes(const LaunchParams &p) {
-    // blob + per-sphere camera terms (16 B) and footprint (16 B) + per-box camera terms
-    return (static_cast<size_t>(p.blob_units) + 2 * static_cast<size_t>(p.n_spheres) + p.n_boxes) * sizeof(float4);
+    // blob + one view's records: per-sphere camera terms (16 B; not with
+    // lean views) and footprint (16 B) + per-box camera terms
+    return (static_cast<size_t>(p.blob_units) + view_units(p)) * sizeof(float4);
 }
 
 int queued_views(const LaunchParams &p, int max_depth) {

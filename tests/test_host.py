@@ -326,7 +326,7 @@ def test_inv_sqrt_near_one():
 # once measured (DESIGN.md §3 keeps the numbers)
 KERNEL_SWITCHES = ["", "-DRT_STATS", "-DRT_CYCLES", "-DRT_PHASE_TRACE", "-DRT_ABLATE_SHADOW", "-DRT_ABLATE_PHONG",
                    "-DRT_ABLATE_TRACE", "-DRT_ABLATE_RAYGEN", "-DRT_ABLATE_FRAMES", "-DRT_WPE0=7",
-                   "-DRT_WPE_DEEP=5", "-DRT_WPE2=7", "-DRT_GMASK_TEXELS=32",
+                   "-DRT_WPE_DEEP=5", "-DRT_WPE2=7", "-DRT_WPE_WIDE=6", "-DRT_GMASK_TEXELS=32",
                    "-DRT_WPE0_MC=7", "-DRT_FAST_MATH", "-DRT_FAST_DIV", "-DRT_FAST_RSQ",
                    "-DRT_FAST_SQRT", "-DRT_FAST_POW", "-DRT_UNIFORM_MAT", "-DRT_ABLATE_BOX_PRIMARY",
                    "-DRT_ABLATE_BOX_SHADOW"]
