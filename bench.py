@@ -42,7 +42,7 @@ launch). The total work of a step is fixed: strong scaling.
 config3 at N=1 (3840x2160 / 64 spheres / depth 2): a step is
 F frames of the animated loop (--frames, default: the views one queued
 launch holds for this scene, every view's frame constants beside the scene
-in LDS — 5 at the depth-2 kernel's 7 waves per SIMD, 7 at round 5's 6),
+in LDS: 7),
 rendered in one rt_render_batch launch whose wave tiles are taken
 view after view from the queues, so the launch's tail is paid once per F
 frames; `single_frame` is the same frames one per launch.
@@ -136,8 +136,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config2")
     ap.add_argument("--frames", type=int, default=None,
-                    help="config2 (default 256) and config3 at N=1 (default: the views one queued launch holds, 5 at "
-                         "7 waves per SIMD): animated frames per step, up to "
+                    help="config2 (default 256) and config3 at N=1 (default: the views one queued launch holds, 7): "
+                         "animated frames per step, up to "
                          "256 per rt_render_batch call (SURVEY.md §8(f) row 3); with all_to_all / none: frames per GPU")
     ap.add_argument("--frame-exchange", choices=["spread", "gather", "all_to_all", "none"], default="spread",
                     help="config2 at N>1: spread (default) = every frame of the step row-tiled over the ranks, "

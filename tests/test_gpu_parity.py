@@ -931,10 +931,9 @@ def test_config5_monte_carlo_kernel_full_frame(gpu_ctx):
 
 
 def test_split_deep_batch_is_counted_and_timed_whole(gpu_ctx):
-    """A deep batch larger than one queued launch holds (5 views of the
-    64-sphere scene at the depth-2 kernel's 7 waves per SIMD) runs as several
-    launches: rt_batch_launches says how many, and rt_last_kernel_ms covers
-    all of them, not the last one only."""
+    """A deep batch larger than one queued launch holds (7 views of the
+    64-sphere scene) runs as several launches: rt_batch_launches says how
+    many, and rt_last_kernel_ms covers all of them, not the last one only."""
     objs = scenes.bench_objects(64)
     w, h, depth = 1280, 720, 2
     sc = rt.Scene(gpu_ctx, objs)
