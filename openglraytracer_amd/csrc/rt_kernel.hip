@@ -1923,6 +1923,12 @@ constexpr bool kQueuedDepth(int depth) { return depth >= 2; }
 template <int kDepth, bool kAccum, bool kDev = false, int kShape = 0>
 __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    // A wave in its prologue (kernel arguments, the scene into LDS, the
+    // barrier) issues ahead of the older waves of its SIMD, which the arbiter
+    // otherwise favours by age; back to 0 after the barrier. Depth-0
+    // batches -1.4 % (config 2, shipped), one frame per launch -2.1 %, any
+    // level above 0 alike (profiles/r06ze_ab_prio.log, r06zf_ab_prio_levels.log).
+    __builtin_amdgcn_s_setprio(1);
     const bool queued = kQueuedDepth(kDepth) && !kDev && p.sched != nullptr;
     const int z = queued ? 0 : static_cast<int>(blockIdx.z);
     const int n_staged = queued ? p.n_views : 1;  // views whose constants this work-group stages
@@ -2003,6 +2009,7 @@ __global__ __launch_bounds__(kThreads) RT_OCCUPANCY void render_kernel(LaunchPar
     if (lane == 0) rt_cyc_cur[wave] = kCycPrologue;
 #endif
     __syncthreads();
+    __builtin_amdgcn_s_setprio(0);
     RT_PHASE(13);
     Scene S;
     S.sph = lds + p.off_spheres;
