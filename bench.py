@@ -167,6 +167,8 @@ def parse():
                     help="N=1: skip the secondary two-stream (`pipelined`) measurement")
     ap.add_argument("--no-rgba8", action="store_true",
                     help="config2 at N=1: skip the same-surface (GL_RGBA8) measurement")
+    ap.add_argument("--no-general", action="store_true",
+                    help="config2, shipped at N=1: skip the general-kernel (scene shapes off) measurement")
     ap.add_argument("--no-single-frame", action="store_true",
                     help="config2, config3 at N=1: skip the one-frame-per-launch measurement (profiling runs: one launch shape)")
     return ap.parse_args()
@@ -1037,6 +1039,31 @@ def main():
             "roofline_frac_float4_equivalent": round(px8 * 16 / (k8 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
         surface("rgba32f")
         del r8
+    if batched and wl in ("config2", "shipped") and world == 1 and rank == 0 and not args.no_general:
+        # the same F frames through the general depth-0 kernel (the scene's
+        # features read at run time, RT_OPT_SCENE_SHAPES off): what a scene
+        # outside the compiled shapes pays per primary ray (DESIGN.md §3,
+        # "Scene shapes"); frame 0 compared with the shaped kernel's frame 0
+        gp = batch_plan("none", "rgba32f")
+        ctx.set_scene_shapes(False)
+        try:
+            eg, kg, _ = measure(gp, args.steps, args.warmup)
+            torch.cuda.synchronize()
+            gen0 = gp.bufs[0][: W * H * 4].clone()
+        finally:
+            ctx.set_scene_shapes(True)
+        gp.render(gp.bufs[0])
+        torch.cuda.synchronize()
+        same0 = bool(torch.equal(gen0, gp.bufs[0][: W * H * 4]))
+        fr = gp.px_per_launch // (W * H)
+        extra["general_kernel"] = {
+            "value": round(gp.rays_per_step * args.steps / eg / 1e6, 3), "unit": "Mrays/s",
+            "kernel_ms": round(kg, 5), "us_per_frame": round(kg / fr * 1e3, 3), "frames_per_launch": fr,
+            "vs_shaped": round(kg / avg_kernel_ms, 4), "frame0_identical_to_shaped": same0,
+            "note": "RT_OPT_SCENE_SHAPES off: the general depth-0 kernel on the same frames"}
+        if not same0:
+            raise SystemExit("general kernel: frame 0 differs from the shaped kernel's")
+        del gp, gen0
     ms_per_step = elapsed / args.steps * 1e3
     value = plan.rays_per_step * args.steps / elapsed / 1e6
     # time basis of the roofline: the kernel's own launch duration when each

@@ -241,6 +241,11 @@ def test_config2_one_gpu_line_checks_itself():
     assert 0.97 <= ratio8 <= 1.01, ratio8
     one = line["single_frame"]
     assert len(one["repeats_us"]) == 3 and len(one["two_streams"]["repeats_us"]) == 3
+    # the general depth-0 kernel (scene shapes off) on the same frames: the
+    # same frame, at a bounded price ("Scene shapes")
+    gk = line["general_kernel"]
+    assert gk["frame0_identical_to_shaped"] and gk["frames_per_launch"] == cfg["frames_per_launch"]
+    assert 1.0 <= gk["vs_shaped"] <= 1.5, gk
 
 
 STUB_RANK = r'''

@@ -12,7 +12,7 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 args=("$@")
 [ ${#args[@]} -eq 0 ] && args=(--steps 50 --warmup 5)
-args+=(--no-single-frame --no-rgba8 --no-pipelined --no-verify)  # one launch shape per profile: no one-frame, RGBA8, pipelined or verification launches
+args+=(--no-single-frame --no-rgba8 --no-pipelined --no-general --no-verify)  # one launch shape per profile: no one-frame, RGBA8, pipelined, general-kernel or verification launches
 run() { timeout -k 10 300 "$@"; }
 pmc() { local name=$1; shift; timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d "$out" -o "$name" -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_$name.log" 2>&1; }
 run rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o trace -- python3 bench.py --no-cpu-baseline "${args[@]}" > "$out/bench_trace.log" 2>&1
