@@ -245,7 +245,7 @@ def test_config2_one_gpu_line_checks_itself():
     # same frame, at a bounded price ("Scene shapes")
     gk = line["general_kernel"]
     assert gk["frame0_identical_to_shaped"] and gk["frames_per_launch"] == cfg["frames_per_launch"]
-    assert 1.0 <= gk["vs_shaped"] <= 1.5, gk
+    assert 1.0 <= gk["vs_shaped"] <= 1.6, gk  # measured 1.42 (r06zi)
 
 
 STUB_RANK = r'''
